@@ -1,0 +1,235 @@
+// amh_capi.hip -- the extern "C" boundary of libamh.so (include/amh.h).
+// Validates arguments, keeps per-handle configuration and model binding, and
+// enqueues the kernels of amh_kernels.hip on the caller's stream.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <new>
+#include <string>
+
+#include "../../include/amh.h"
+#include "../../include/amh_math.h"
+#include "amh_internal.h"
+
+#include <vector>
+
+struct amh_handle {
+  amh_config cfg;
+  int device = 0;
+  int model_id = 0;
+  amh::ModelArgs model{nullptr, 0, 0};
+  int64_t n_data = 0;
+  float* gamma_tab = nullptr;  // device, kGammaTab entries
+  std::string err;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(amh_handle* h, int code, const std::string& msg) {
+  if (h) h->err = msg; else g_err = msg;
+  return code;
+}
+
+int hip_fail(amh_handle* h, hipError_t e, const char* where) {
+  return fail(h, AMH_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+bool state_ok(const amh_state* s) {
+  return s && s->i && s->z && s->potential_energy && s->mean_accept_prob && s->loc && s->scale &&
+         s->log_step_size && s->as_change && s->rng_key;
+}
+
+int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d, std::string* why) {
+  switch (model_id) {
+    case AMH_MODEL_GAUSSIAN:
+      if (n_data != (int64_t)d + (int64_t)d * d + 1) { *why = "gaussian data must hold d + d*d + 1 floats"; return -1; }
+      return d;
+    case AMH_MODEL_EIGHT_SCHOOLS: {
+      if (nip < 1) { *why = "eight_schools needs iparams {J}"; return -1; }
+      const int64_t J = ip[0];
+      if (n_data != 3 * J) { *why = "eight_schools data must hold 3*J floats"; return -1; }
+      return (int)(J + 2);
+    }
+    case AMH_MODEL_KIDIQ: {
+      if (nip < 1) { *why = "kidiq needs iparams {N}"; return -1; }
+      if (n_data != 3 * ip[0]) { *why = "kidiq data must hold 3*N floats"; return -1; }
+      return 4;
+    }
+    case AMH_MODEL_DIAMONDS: {
+      if (nip < 2) { *why = "diamonds needs iparams {N, K}"; return -1; }
+      const int64_t N = ip[0], K = ip[1];
+      if (n_data != N * (K - 1) + N) { *why = "diamonds data must hold N*(K-1) + N floats"; return -1; }
+      return (int)(K + 1);
+    }
+    default:
+      *why = "unknown model id";
+      return -1;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+int amh_version(void) { return AMH_ABI_VERSION; }
+
+const char* amh_last_error(const amh_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int amh_create(const amh_config* cfg, int device, amh_handle** out) {
+  if (!cfg || !out) return fail(nullptr, AMH_EINVAL, "amh_create: null argument");
+  if (cfg->dim < 1 || cfg->dim > 64) return fail(nullptr, AMH_EINVAL, "amh_create: dim must be in [1, 64]");
+  if (cfg->num_warmup < 0) return fail(nullptr, AMH_EINVAL, "amh_create: num_warmup < 0");
+  amh_handle* h = new (std::nothrow) amh_handle();
+  if (!h) return fail(nullptr, AMH_ENOMEM, "amh_create: out of memory");
+  h->cfg = *cfg;
+  h->device = device;
+  // gamma_n = 1 / n^a for n < kGammaTab, evaluated on the host by the same
+  // routine the kernels use for larger n (include/amh_math.h).
+  std::vector<float> tab(amh::kGammaTab);
+  tab[0] = 1.0f;
+  for (int32_t n = 1; n < amh::kGammaTab; ++n) tab[n] = amh_lr_gamma(n, cfg->lr_decay);
+  hipError_t e = hipSetDevice(device);
+  if (e == hipSuccess) e = hipMalloc(&h->gamma_tab, sizeof(float) * tab.size());
+  if (e == hipSuccess) e = hipMemcpy(h->gamma_tab, tab.data(), sizeof(float) * tab.size(), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    const int rc = hip_fail(nullptr, e, "amh_create");
+    if (h->gamma_tab) (void)hipFree(h->gamma_tab);
+    delete h;
+    return rc;
+  }
+  *out = h;
+  return AMH_OK;
+}
+
+int amh_destroy(amh_handle* h) {
+  if (h && h->gamma_tab) {
+    (void)hipSetDevice(h->device);
+    (void)hipFree(h->gamma_tab);
+  }
+  delete h;
+  return AMH_OK;
+}
+
+int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n_data, const int64_t* iparams,
+                   int32_t n_iparams) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_bind_model: null handle");
+  if (!data) return fail(h, AMH_EINVAL, "amh_bind_model: null data");
+  std::string why;
+  const int dm = expected_dim(model_id, n_data, iparams, n_iparams, h->cfg.dim, &why);
+  if (dm < 0) return fail(h, AMH_EINVAL, "amh_bind_model: " + why);
+  if (dm != h->cfg.dim)
+    return fail(h, AMH_EINVAL, "amh_bind_model: model dimension " + std::to_string(dm) + " != config dim " +
+                                   std::to_string(h->cfg.dim));
+  h->model_id = model_id;
+  h->model.data = data;
+  h->model.n = (model_id == AMH_MODEL_KIDIQ || model_id == AMH_MODEL_DIAMONDS) ? iparams[0] : 0;
+  h->model.k = (model_id == AMH_MODEL_DIAMONDS) ? iparams[1] : 0;
+  h->n_data = n_data;
+  return AMH_OK;
+}
+
+int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t num_chains, const float* init_z,
+             const amh_state* out, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_init: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_init: no model bound");
+  if (!key || !state_ok(out) || num_chains < 1 || chain_offset < 0)
+    return fail(h, AMH_EINVAL, "amh_init: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_init/hipSetDevice");
+  amh::InitParams p{};
+  p.out = *out;
+  p.C = num_chains;
+  p.chain_offset = chain_offset;
+  p.d = h->cfg.dim;
+  p.key0 = key[0];
+  p.key1 = key[1];
+  p.init_z = init_z;
+  p.model = h->model;
+  e = amh::run_init(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_init");
+  return AMH_OK;
+}
+
+int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out, int32_t n_steps,
+             const amh_collect* collect, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_step: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_step: no model bound");
+  if (!state_ok(in) || !state_ok(out) || num_chains < 1 || n_steps < 0)
+    return fail(h, AMH_EINVAL, "amh_step: bad arguments");
+  if (n_steps == 0) return AMH_OK;
+  if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_step: thinning must be >= 1");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_step/hipSetDevice");
+  amh::StepParams p{};
+  p.in = *in;
+  p.out = *out;
+  p.C = num_chains;
+  p.d = h->cfg.dim;
+  p.W = h->cfg.num_warmup;
+  p.a = h->cfg.lr_decay;
+  p.target = h->cfg.target_accept_prob;
+  p.eps = h->cfg.eps;
+  p.n_steps = n_steps;
+  p.thinning = collect ? collect->thinning : 1;
+  p.col_z = collect ? collect->z : nullptr;
+  p.col_pe = collect ? collect->potential_energy : nullptr;
+  p.accept_count = collect ? collect->accept_count : nullptr;
+  p.gamma_tab = h->gamma_tab;
+  p.gamma_tab_n = amh::kGammaTab;
+  p.model = h->model;
+  e = amh::run_step(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_step");
+  return AMH_OK;
+}
+
+int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_potential: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_potential: no model bound");
+  if (!z || !pe || n < 1) return fail(h, AMH_EINVAL, "amh_potential: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_potential/hipSetDevice");
+  amh::PotParams p{z, pe, n, h->cfg.dim, h->model};
+  e = amh::run_potential(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_potential");
+  return AMH_OK;
+}
+
+int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t n_points, int64_t n_samples,
+                   const float* loc, const float* scale_packed, float log_step_size, int32_t n, float* out,
+                   void* stream) {
+  (void)loc;  // the frozen kernel's proposal does not read the mean (arwmh.py:166-167)
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_sample_pnx: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_sample_pnx: no model bound");
+  if (!key || !x || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
+    return fail(h, AMH_EINVAL, "amh_sample_pnx: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
+  amh::PnxParams p{};
+  p.x = x;
+  p.n_points = n_points;
+  p.n_samples = n_samples;
+  p.scale = scale_packed;
+  p.log_step_size = log_step_size;
+  p.eps = h->cfg.eps;
+  p.n = n;
+  p.d = h->cfg.dim;
+  p.key0 = key[0];
+  p.key1 = key[1];
+  p.out = out;
+  p.model = h->model;
+  e = amh::run_pnx(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx");
+  return AMH_OK;
+}
+
+int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint32_t* out, void* stream) {
+  if (!key || !out || n < 1 || chain_offset < 0) return fail(nullptr, AMH_EINVAL, "amh_chain_keys: bad arguments");
+  hipError_t e = amh::run_chain_keys(key[0], key[1], chain_offset, n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "amh_chain_keys");
+  return AMH_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,72 @@
+// amh_internal.h -- kernel parameter blocks shared by amh_kernels.hip and the
+// C-ABI layer amh_capi.hip.  Not part of the public ABI (include/amh.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/amh.h"
+
+namespace amh {
+
+// Learning-rate table size: gamma_n for n < 2^20 is precomputed on the host
+// with the same amh_lr_gamma the device would run (bit-identical); larger n
+// fall back to the device routine.
+constexpr int32_t kGammaTab = 1 << 20;
+
+struct ModelArgs {
+  const float* data;  // device, model-specific layout (include/amh.h)
+  int64_t n;          // N rows (regression models)
+  int64_t k;          // K columns (diamonds)
+};
+
+struct StepParams {
+  amh_state in, out;
+  int64_t C;
+  int32_t d, W;
+  float a, target, eps;
+  int32_t n_steps;
+  float* col_z;            // [n_keep][C][d] or null
+  float* col_pe;           // [n_keep][C] or null
+  int32_t* accept_count;   // [C] or null
+  int32_t thinning;
+  const float* gamma_tab;  // gamma_n = amh_lr_gamma(n, a) for n < gamma_tab_n
+  int32_t gamma_tab_n;
+  ModelArgs model;
+};
+
+struct InitParams {
+  amh_state out;
+  int64_t C, chain_offset;
+  int32_t d;
+  uint32_t key0, key1;
+  const float* init_z;
+  ModelArgs model;
+};
+
+struct PotParams {
+  const float* z;
+  float* pe;
+  int64_t n;
+  int32_t d;
+  ModelArgs model;
+};
+
+struct PnxParams {
+  const float* x;
+  int64_t n_points, n_samples;
+  const float* scale;  // packed shared factor
+  float log_step_size, eps;
+  int32_t n, d;
+  uint32_t key0, key1;
+  float* out;
+  ModelArgs model;
+};
+
+hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);
+hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
+hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
+hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);
+hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, uint32_t* out,
+                          hipStream_t s);
+
+}  // namespace amh

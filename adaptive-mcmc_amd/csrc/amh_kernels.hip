@@ -1,0 +1,891 @@
+// amh_kernels.hip -- gfx950 (CDNA4) kernels for the ARWMH hot path.
+//
+// Reference: savelovme/adaptive-mcmc python/kernels/arwmh.py (ARWMH.sample
+// :140-207, ARWMH.init :84-138, ARWMH.sample_Pnx :230-270) and the NumPyro
+// rank-one cholesky_update it calls at :190.  This is not a translation: the
+// reference runs one chain per XLA:CPU program; here one wavefront lane-group
+// owns one chain and the whole transition (RNG, proposal, potential, accept,
+// mean / Cholesky / step-size adaptation) runs in registers.
+//
+// Lane mapping ("lane = row"): a chain of dimension d <= DMAX is owned by a
+// group of G = DMAX lanes (G in {1,..,64}); lane r holds row r of the packed
+// lower-triangular factor L in DMAX registers A[0..DMAX-1] (A[j] = L_rj, zero
+// above the diagonal), plus z_r, mu_r and the per-column scalars of the
+// rank-one update.  Column j of L is stored contiguously in HBM (packed,
+// column-major), so the load of register j is one coalesced dword access over
+// lanes j..d-1 -- no LDS staging and no transposition.
+//
+// Bit spec: the arithmetic order here is mirrored exactly by the C oracle
+// oracle/amh_oracle.c; both compile with -ffp-contract=off and take every
+// transcendental from include/amh_math.h.  See DESIGN.md "bit spec".
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "../../include/amh.h"
+#include "../../include/amh_math.h"
+#include "amh_internal.h"
+
+namespace amh {
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// ------------------------------------------------------------ lane groups --
+// Cross-lane primitives inside a group of G lanes (G | 64), built on DPP,
+// ds_swizzle, permlane and readlane so that no lane-address VGPRs are needed.
+// Their association orders are part of the bit spec (oracle: group_sum,
+// group_excl_scan).
+namespace dpp {
+constexpr int quad(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+constexpr int kRowShr0 = 0x110;
+constexpr int kRowRor0 = 0x120;
+constexpr int kWaveShr1 = 0x138;
+constexpr int kRowBcast15 = 0x142;
+constexpr int kRowBcast31 = 0x143;
+constexpr int kRowNewBcast0 = 0x150;
+}  // namespace dpp
+
+// compile-time unrolled loop: f(std::integral_constant<int, j>) for j < N
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int CTRL, int ROWMASK = 0xF, bool BC = true>
+__device__ __forceinline__ float dppf(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWMASK, 0xF, BC));
+}
+template <int PATTERN>
+__device__ __forceinline__ float swz(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), PATTERN));
+}
+
+template <int G>
+struct Grp {
+  static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group width must be a power of two");
+  static __device__ __forceinline__ int r() { return lane_id() & (G - 1); }
+
+  // value of lane J of this lane's group
+  template <int J>
+  static __device__ __forceinline__ float bcast(float v) {
+    static_assert(J >= 0 && J < G, "lane index out of group");
+    if constexpr (G == 64) {
+      return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), J));
+    } else if constexpr (G == 32) {
+      const int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::kRowNewBcast0 + (J & 15), 0xF, 0xF, false);
+      const auto sw = __builtin_amdgcn_permlane16_swap(t, t, false, false);
+      return __int_as_float(J < 16 ? sw[0] : sw[1]);
+    } else if constexpr (G == 16) {
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::kRowNewBcast0 + J, 0xF, 0xF, false));
+    } else if constexpr (G == 8) {
+      return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (J << 5)));
+    } else if constexpr (G == 4) {
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::quad(J, J, J, J), 0xF, 0xF, false));
+    } else if constexpr (G == 2) {
+      return __int_as_float(
+          __builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::quad(J, J, 2 + J, 2 + J), 0xF, 0xF, false));
+    } else {
+      return v;
+    }
+  }
+  template <int J>
+  static __device__ __forceinline__ uint32_t bcast_u(uint32_t v) {
+    return (uint32_t)__float_as_int(bcast<J>(__int_as_float((int)v)));
+  }
+  // runtime lane index (model code with data-dependent layout)
+  static __device__ __forceinline__ float bcast_rt(float v, int j) {
+    if constexpr (G == 64) {
+      return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+    } else if constexpr (G == 1) {
+      return v;
+    } else {
+      return __shfl(v, (lane_id() & ~(G - 1)) | j, 64);
+    }
+  }
+
+  // butterfly: for off = 1, 2, 4, ..: x_r = x_r + x_{r ^ off}  (oracle: group_sum)
+  static __device__ __forceinline__ float sum(float v) {
+    if constexpr (G >= 2) v = v + dppf<dpp::quad(1, 0, 3, 2)>(0.0f, v);
+    if constexpr (G >= 4) v = v + dppf<dpp::quad(2, 3, 0, 1)>(0.0f, v);
+    if constexpr (G >= 8) v = v + swz<0x1F | (4 << 10)>(v);
+    if constexpr (G >= 16) v = v + dppf<dpp::kRowRor0 + 8>(0.0f, v);
+    if constexpr (G >= 32) v = v + swz<0x1F | (16 << 10)>(v);
+    if constexpr (G == 64) {
+      // every lane of each 32-lane half holds that half's total here
+      v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    }
+    return v;
+  }
+
+  // exclusive scan (oracle: group_excl_scan): shift by one lane, inclusive
+  // Hillis-Steele inside 16-lane rows, then row totals via row_bcast15/31.
+  static __device__ __forceinline__ float excl_scan(float t, int rr) {
+    if constexpr (G == 1) {
+      return 0.0f;
+    } else {
+      float x = dppf<dpp::kWaveShr1>(0.0f, t);
+      if constexpr (G < 64) x = (rr == 0) ? 0.0f : x;
+      if constexpr (G >= 2) { const float y = dppf<dpp::kRowShr0 + 1>(0.0f, x); x = (G >= 16 || rr >= 1) ? x + y : x; }
+      if constexpr (G >= 4) { const float y = dppf<dpp::kRowShr0 + 2>(0.0f, x); x = (G >= 16 || rr >= 2) ? x + y : x; }
+      if constexpr (G >= 8) { const float y = dppf<dpp::kRowShr0 + 4>(0.0f, x); x = (G >= 16 || rr >= 4) ? x + y : x; }
+      if constexpr (G >= 16) { const float y = dppf<dpp::kRowShr0 + 8>(0.0f, x); x = x + y; }
+      if constexpr (G >= 32) { x = x + dppf<dpp::kRowBcast15, 0xA>(0.0f, x); }
+      if constexpr (G == 64) { x = x + dppf<dpp::kRowBcast31, 0xC>(0.0f, x); }
+      return x;
+    }
+  }
+
+  static __device__ __forceinline__ bool any(bool p) {
+    const unsigned long long m = __ballot(p);
+    if constexpr (G == 64) {
+      return m != 0ull;
+    } else {
+      const int g0 = lane_id() & ~(G - 1);
+      constexpr unsigned long long gm = (1ull << G) - 1ull;
+      return ((m >> g0) & gm) != 0ull;
+    }
+  }
+};
+
+// packed column-major lower triangle: column j starts at j*d - j(j-1)/2
+__device__ __forceinline__ int64_t col_off(int d, int j) {
+  return (int64_t)j * d - (int64_t)j * (j - 1) / 2;
+}
+
+#define HALF_LOG_2PI 0.918938533204672742f
+
+// ------------------------------------------------------------------ models --
+// Every model: static potential(x_r, r, d, args, lds) -> U (same value in all
+// lanes of the group), evaluated with all lanes converged.
+
+template <int G>
+struct GaussianM {
+  // data = [m (d) | P (d*d) | c0].  P is symmetric; LDS holds row r of P at
+  // lds[r * ld + j] with ld = d rounded up to 4 plus 4 floats of padding, so
+  // lane r reads its own row with ds_read_b128 (4 columns per read) and the
+  // 16-B slots of the 16 lanes of a read group fall on distinct banks.
+  static __host__ __device__ int ld(int d) { return ((d + 3) & ~3) + 4; }
+  static size_t lds_bytes(int d) { return (size_t)d * ld(d) * sizeof(float); }
+  static __device__ void stage(float* lds, const ModelArgs& m, int d) {
+    const float* P = m.data + d;
+    const int L = ld(d);
+    for (int k = threadIdx.x; k < d * L; k += blockDim.x) {
+      const int row = k / L, col = k - row * L;
+      lds[k] = (col < d) ? P[row * d + col] : 0.0f;
+    }
+  }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
+                                                    const float* lds) {
+    const bool act = r < d;
+    const float mr = act ? m.data[r] : 0.0f;
+    const float diff = act ? x - mr : 0.0f;
+    const float4* prow = reinterpret_cast<const float4*>(lds + (act ? r : 0) * ld(d));
+    float y = 0.0f;
+    static_for<(G + 3) / 4>([&](auto J4) {
+      constexpr int j4 = J4;
+      if (4 * j4 < d) {
+        const float4 pv = prow[j4];
+        const float pj[4] = {pv.x, pv.y, pv.z, pv.w};
+        static_for<4>([&](auto K) {
+          constexpr int j = 4 * j4 + K;
+          if constexpr (j < G) {
+            if (j < d) y = fmaf(act ? pj[K] : 0.0f, Grp<G>::template bcast<j>(diff), y);
+          }
+        });
+        if ((j4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound LDS reads in flight
+      }
+    });
+    const float q = act ? diff * y : 0.0f;
+    const float S = Grp<G>::sum(q);
+    return (0.5f * S) + m.data[d + d * d];
+  }
+};
+
+template <int G>
+struct EightSchoolsM {
+  // z = [mu, log tau, theta_base (J)]; data = [y (J) | sigma (J) | log sigma (J)]
+  static size_t lds_bytes(int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
+                                                    const float*) {
+    const int J = d - 2;
+    const float mu = Grp<G>::template bcast<0>(x);
+    const float lt = Grp<G>::template bcast<1>(x);
+    const float tau = amh_expf(lt);
+    float v = 0.0f;
+    if (r == 0) {
+      const float t = mu / 5.0f;
+      v = ((-0.5f * (t * t)) - 1.60943791243410037f) - HALF_LOG_2PI;
+    } else if (r == 1) {
+      const float t = tau / 5.0f;
+      v = ((-0.451582705289454865f - 1.60943791243410037f) - amh_log1pf(t * t)) + lt;
+    } else if (r < d) {
+      const int j = r - 2;
+      const float th = x;
+      const float lpt = (-0.5f * (th * th)) - HALF_LOG_2PI;
+      const float e = (m.data[j] - (mu + tau * th)) / m.data[J + j];
+      const float lpy = ((-0.5f * (e * e)) - m.data[2 * J + j]) - HALF_LOG_2PI;
+      v = lpt + lpy;
+    }
+    return -Grp<G>::sum(v);
+  }
+};
+
+template <int G>
+struct KidiqM {
+  // z = [beta0, beta1, beta2, log sigma]; data = [kid | hs | iq] (N each)
+  static size_t lds_bytes(int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ float potential(float x, int r, int, const ModelArgs& m,
+                                                    const float*) {
+    const int64_t N = m.n;
+    const float b0 = Grp<G>::template bcast<0>(x), b1 = Grp<G>::template bcast<1>(x);
+    const float b2 = Grp<G>::template bcast<2>(x), ls = Grp<G>::template bcast<3>(x);
+    const float sg = amh_expf(ls);
+    const float isg = 1.0f / sg;
+    const float* kid = m.data;
+    const float* hs = m.data + N;
+    const float* iq = m.data + 2 * N;
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      const float mu = fmaf(b2, iq[n], fmaf(b1, hs[n], b0));
+      const float e = (kid[n] - mu) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    const float S = Grp<G>::sum(acc);
+    const float t = sg / 2.5f;
+    const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpr = ((-0.451582705289454865f - 0.916290731874155065f) - amh_log1pf(t * t)) + ls;
+    return -(ll + lpr);
+  }
+};
+
+__device__ __forceinline__ float lp_student3(float x, float loc, float scale, float c) {
+  const float t = (x - loc) / scale;
+  return c - 2.0f * amh_log1pf((t * t) / 3.0f);
+}
+
+template <int G>
+struct DiamondsM {
+  // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)]
+  // Straight VALU restatement (parity path); the MFMA GEMM path lives in
+  // amh_diamonds.hip.
+  static size_t lds_bytes(int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
+                                                    const float*) {
+    const int64_t N = m.n;
+    const int Kc = d - 2;
+    const float* X = m.data;
+    const float* Y = m.data + N * Kc;
+    float xb[G];
+    static_for<G>([&](auto J) { xb[J] = Grp<G>::template bcast<J>(x); });
+    const float icpt = xb[0];
+    const float ls = Grp<G>::bcast_rt(x, Kc + 1);
+    const float sg = amh_expf(ls);
+    const float isg = 1.0f / sg;
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      float mu = 0.0f;
+#pragma unroll
+      for (int k = 0; k < G - 1; ++k) {
+        if (k >= Kc) continue;
+        mu = fmaf(X[n * Kc + k], xb[1 + k], mu);
+      }
+      const float e = (Y[n] - (icpt + mu)) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    const float S = Grp<G>::sum(acc);
+    const float bb = (r >= 1 && r <= Kc) ? x * x : 0.0f;
+    const float B = Grp<G>::sum(bb);
+    const float cst = -3.30347394261755545f;
+    const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+    const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+    const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+    return -(((ll + lpb) + lpi) + lps);
+  }
+};
+
+// --------------------------------------------------------------- geometry --
+constexpr int kBlock = 256;  // 4 waves
+
+template <int G>
+struct Geo {
+  static constexpr int CPW = 64 / G;  // chains per wave
+};
+
+// Chain owned by this lane's group for work item `item`; clamped to C-1 so
+// that tail groups run converged on valid memory and simply do not store.
+template <int G>
+__device__ __forceinline__ int64_t item_chain(int64_t item) {
+  int64_t c = item * Geo<G>::CPW + (lane_id() / G);
+  if constexpr (G == 64) c = (int64_t)__builtin_amdgcn_readfirstlane((int)c);  // wave-uniform
+  return c;
+}
+
+// gamma_n beyond the host-built table (n >= 2^20): same bits, kept out of line
+// so its double-precision constants do not occupy registers in the step loop.
+__device__ __noinline__ float lr_gamma_slow(int32_t n, float a) { return amh_lr_gamma(n, a); }
+
+// ------------------------------------------------------------ buffer I/O --
+// Raw buffer descriptor over one wave's chain block: the base is wave-uniform
+// (SGPRs), per-lane offsets are 32-bit VGPRs and the per-column part of an
+// offset is an SGPR, so the 64 column loads of a chain share one VGPR.  Lanes
+// that must not touch memory get an out-of-range voffset (loads return 0,
+// stores are dropped by the hardware range check).
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct Buf {
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ Buf(const void* base, uint32_t bytes) {
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  }
+  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, 0));
+  }
+  __device__ __forceinline__ void st(float v, uint32_t voff, uint32_t soff) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, 0);
+  }
+};
+
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (const void*)(((uint64_t)hi << 32) | lo);
+}
+
+// v_writelane through the LLVM intrinsic (no clang builtin in ROCm 7.2)
+__device__ int amh_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// lane J of the group takes `v` (uniform in the group), other lanes keep `old`
+template <int G, int J>
+__device__ __forceinline__ float capture(float old, float v, int rr) {
+  if constexpr (G == 64) {
+    return __int_as_float(amh_writelane_i32(__float_as_int(v), J, __float_as_int(old)));
+  } else {
+    return (rr == J) ? v : old;
+  }
+}
+
+// -------------------------------------------------------------- step kernel --
+// One or more ARWMH transitions (arwmh.py:140-207) per chain with the state
+// held in registers between steps.
+//
+// Between steps the factor lives in registers in unit-lower form: U[j] holds
+// U_rj = L_rj / L_jj (U_rr = 1 exactly, zero above the diagonal) and `dl`
+// holds L_rr.  numpyro's cholesky_update works on exactly this pair (it
+// divides the scaled factor by its diagonal, arwmh.py:190), so the update
+// needs no per-column masks: the w_r of a row is zeroed exactly when its own
+// column passes (w - w*1), which keeps the upper triangle at exact zeros.
+// L = U diag(dl) is formed only when the state is written back.
+template <int DMAX, template <int> class M, bool EXACT>
+__global__ __launch_bounds__(kBlock) void arwmh_step_kernel(StepParams p) {
+  constexpr int G = DMAX;
+  constexpr int CPW = Geo<G>::CPW;
+  using Gp = Grp<G>;
+  extern __shared__ float lds[];
+  const int d = EXACT ? DMAX : p.d;
+  M<G>::stage(lds, p.model, d);
+  __syncthreads();
+
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.C;
+  const uint32_t P = (uint32_t)(d * (d + 1) / 2);
+  const int64_t item = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t first = (int64_t)__builtin_amdgcn_readfirstlane((int)(item * CPW));
+  if (first >= C) return;  // whole wave past the end (wave-uniform)
+  const int64_t chain = first + lane_id() / G;
+  const bool chain_ok = chain < C;
+  const int64_t cl = chain_ok ? chain : C - 1;
+  const uint32_t gsub = (uint32_t)(cl - first);  // group's chain within the wave block
+
+  // wave block of the packed factors, in and out
+  const uint32_t wave_bytes = (uint32_t)CPW * P * 4u;
+  const Buf Lin(uniform_ptr(p.in.scale + first * P), wave_bytes);
+  const Buf Lout(uniform_ptr(p.out.scale + first * P), wave_bytes);
+  const uint32_t vrow = (gsub * P + (uint32_t)r) * 4u;  // lane's row offset (column 0)
+
+  // ---- load state
+  float U[DMAX];
+  float dl, inv;
+  {
+    const uint32_t dofs = act ? (gsub * P + (uint32_t)col_off(d, r)) * 4u : kOOB;
+    dl = Lin.ld(dofs, 0);
+    inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+    static_for<DMAX>([&](auto J) {
+      constexpr int j = J;
+      U[j] = 0.0f;
+      if (j < d) {
+        const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
+        const float x = Lin.ld((r > j && act) ? vrow : kOOB, so);
+        const float ij = Gp::template bcast<j>(inv);
+        U[j] = (r == j) ? 1.0f : x * ij;
+      }
+    });
+  }
+  float z = act ? p.in.z[cl * d + r] : 0.0f;
+  float mu = act ? p.in.loc[cl * d + r] : 0.0f;
+  int32_t it = p.in.i[cl];
+  float pe = p.in.potential_energy[cl];
+  float macc = p.in.mean_accept_prob[cl];
+  float lam = p.in.log_step_size[cl];
+  float asc = p.in.as_change[cl];
+  const uint32_t k0 = p.in.rng_key[2 * cl], k1 = p.in.rng_key[2 * cl + 1];
+  int32_t nacc = 0;
+  bool updated = false;
+
+  for (int32_t t = 0; t < p.n_steps; ++t) {
+    int rr = r;
+    if constexpr (G < 64) asm volatile("" : "+v"(rr));  // keep per-column compares in the loop
+
+    // ---- noise (arwmh.py:162-165, 174): stream position = state.i
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+    const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+    const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+
+    // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
+    //      L xi = U (dl * xi)
+    const float el = amh_expf(lam);
+    const float eta = dl * xi;
+    float acc = 0.0f;
+    static_for<DMAX>([&](auto J) {
+      if (J < d) acc = fmaf(U[J], Gp::template bcast<J>(eta), acc);
+    });
+    const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+
+    // ---- potential, NaN -> +inf (arwmh.py:169-171)
+    float pep = M<G>::potential(zp, r, d, p.model, lds);
+    if (amh_isnan(pep)) pep = INFINITY;
+
+    // ---- accept / reject (arwmh.py:173-178)
+    const float ex = amh_expf(pe - pep);
+    const float alpha = (ex > 1.0f) ? 1.0f : ex;
+    const bool accept = u < alpha;
+    const float zn = accept ? zp : z;
+    const float pen = accept ? pep : pe;
+    nacc += accept ? 1 : 0;
+
+    // ---- schedule (arwmh.py:180-185)
+    const int32_t itr = it + 1;
+    const int32_t n = (it < p.W) ? itr : itr - p.W;
+    const float gamma = (n < p.gamma_tab_n) ? p.gamma_tab[n] : lr_gamma_slow(n, p.a);
+    const float maccn = macc + (alpha - macc) / (float)n;
+
+    // ---- mean and step size (arwmh.py:188-189, 193)
+    const float delta = act ? zn - mu : 0.0f;
+    const float mun = act ? mu + gamma * delta : 0.0f;
+    const float lamn = lam + gamma * (alpha - p.target);
+    const float e1 = amh_expf(lamn);
+
+    // ---- rank-one update of sqrt(1-gamma) L by (delta, gamma)
+    //      (arwmh.py:190-191 -> numpyro cholesky_update), NaN -> keep L.
+    const float sq = sqrtf(1.0f - gamma);
+    const float ajj = sq * dl;
+    const float Dg = ajj * ajj;
+    const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+
+    // sweep 1: w*_j = w_j when column j is applied (forward solve U w* = delta)
+    float w = delta;
+    float ws = 0.0f;
+    static_for<DMAX>([&](auto J) {
+      if (J < d) {
+        const float wj = Gp::template bcast<J>(w);
+        ws = capture<G, J>(ws, wj, rr);
+        w = fmaf(-wj, U[J], w);
+      }
+    });
+
+    // per-column scalars, one column per lane; b_j by exclusive scan
+    const float gw2 = act ? gamma * (ws * ws) : 0.0f;
+    const float tsc = act ? gw2 / Dg : 0.0f;
+    const float b = 1.0f + Gp::excl_scan(tsc, rr);
+    const float g = (b * Dg) + gw2;
+    const float dn = g / b;
+    const float c = (gamma * ws) / g;
+    const float q = sqrtf(dn);
+    const float dnew = fmaf(c, 0.0f, one) * q;  // new diagonal of column r
+
+    const bool revert = Gp::any(act && amh_isnan(dnew));
+    // A NaN anywhere in numpyro's updated factor shows up in its new diagonal
+    // (fmaf(c, 0, U_jj) q_j): c_j, q_j and U_jj = A_jj / A_jj are the only
+    // per-column quantities, and every off-diagonal entry is finite whenever
+    // they are ("keep-L rule").  So the keep-L test of
+    // arwmh.py:191 is decided before the factor is touched.
+    float sacc = 0.0f;
+    if (!revert) {
+      // sweep 2: U'_rj = U_rj + c_j w_r^{(j+1)};  as_change terms
+      //   L'_rj e1 - L_rj e0 = U'_rj (q_j e1) - U_rj (dl_j e0)
+      const float ed = dl * el;
+      const float qe = q * e1;
+      w = delta;
+      static_for<DMAX>([&](auto J) {
+        if (J < d) {
+          const float wj = Gp::template bcast<J>(ws);
+          const float cj = Gp::template bcast<J>(c);
+          const float edj = Gp::template bcast<J>(ed);
+          const float qej = Gp::template bcast<J>(qe);
+          const float uo = U[J];
+          w = fmaf(-wj, uo, w);
+          const float un = fmaf(cj, w, uo);
+          const float told = uo * edj;
+          const float tt = fmaf(un, qej, -told);
+          sacc = fmaf(tt, tt, sacc);
+          U[J] = un;
+        }
+      });
+      asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
+      dl = act ? q : 0.0f;
+      updated = true;
+    }
+    if (revert) {
+      // factor unchanged: as_change = || L (e1 - e0) ||_F
+      const float ed0 = dl * el;
+      const float ed1 = dl * e1;
+      sacc = 0.0f;
+      static_for<DMAX>([&](auto J) {
+        if (J < d) {
+          const float uo = U[J];
+          const float told = uo * Gp::template bcast<J>(ed0);
+          const float tt = fmaf(uo, Gp::template bcast<J>(ed1), -told);
+          sacc = fmaf(tt, tt, sacc);
+        }
+      });
+      asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
+    }
+
+    // ---- commit (arwmh.py:199-207)
+    it = itr;
+    z = zn;
+    pe = pen;
+    macc = maccn;
+    mu = mun;
+    lam = lamn;
+
+    if (p.col_z != nullptr || p.col_pe != nullptr) {
+      if ((t + 1) % p.thinning == 0 && chain_ok) {
+        const int64_t k = t / p.thinning;
+        if (p.col_z != nullptr && act) p.col_z[(k * C + chain) * d + r] = z;
+        if (p.col_pe != nullptr && r == 0) p.col_pe[k * C + chain] = pe;
+      }
+    }
+  }
+
+  // ---- store state: L = U diag(dl); untouched factors are copied verbatim
+  const bool any_upd = Gp::any(updated);
+  int r3 = r;
+  asm volatile("" : "+v"(r3));
+  uint32_t vrow3 = vrow;
+  asm volatile("" : "+v"(vrow3));
+  const bool st_ok = (r3 < d) && chain_ok;
+  static_for<DMAX>([&](auto J) {
+    constexpr int j = J;
+    if (j < d) {
+      const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
+      const uint32_t vo = (r3 >= j && st_ok) ? vrow3 : kOOB;
+      float v;
+      if (any_upd) {
+        v = U[j] * Gp::template bcast<j>(dl);
+      } else {
+        v = Lin.ld(vo, so);
+      }
+      Lout.st(v, vo, so);
+    }
+  });
+  if (chain_ok) {
+    if (act) {
+      p.out.z[chain * d + r] = z;
+      p.out.loc[chain * d + r] = mu;
+    }
+    if (r == 0) {
+      p.out.i[chain] = it;
+      p.out.potential_energy[chain] = pe;
+      p.out.mean_accept_prob[chain] = macc;
+      p.out.log_step_size[chain] = lam;
+      p.out.as_change[chain] = asc;
+      p.out.rng_key[2 * chain] = k0;
+      p.out.rng_key[2 * chain + 1] = k1;
+      if (p.accept_count != nullptr) p.accept_count[chain] += nacc;
+    }
+  }
+}
+
+// -------------------------------------------------------------- init kernel --
+// arwmh.py:84-138 with numpyro init_to_uniform (U(-2,2) per coordinate).
+template <int DMAX, template <int> class M, bool EXACT>
+__global__ __launch_bounds__(kBlock) void arwmh_init_kernel(InitParams p) {
+  constexpr int G = DMAX;
+  using Gp = Grp<G>;
+  extern __shared__ float lds[];
+  const int d = EXACT ? DMAX : p.d;
+  M<G>::stage(lds, p.model, d);
+  __syncthreads();
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.C;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
+  const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t item = wave0; item < n_items; item += wstride) {
+    const int64_t chain = item_chain<G>(item);
+    const bool chain_ok = chain < C;
+    const int64_t cl = chain_ok ? chain : C - 1;
+    const uint64_t gc = (uint64_t)(p.chain_offset + cl);
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)gc, (uint32_t)(gc >> 32), 0u, AMH_TAG_CHAINKEY,
+                                           p.key0, p.key1);
+    float z0 = 0.0f;
+    if (act) {
+      if (p.init_z != nullptr) {
+        z0 = p.init_z[cl * d + r];
+      } else {
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, 0u, 0u, AMH_TAG_INIT, kk.v[0], kk.v[1]);
+        const float v = (amh_unif01_from_bits(o.v[0]) * 4.0f) + (-2.0f);
+        z0 = (v < -2.0f) ? -2.0f : v;
+      }
+    }
+    const float pe0 = M<G>::potential(z0, r, d, p.model, lds);
+    if (chain_ok) {
+      float* Lout = p.out.scale + chain * P;
+      if (act) {
+        p.out.z[chain * d + r] = z0;
+        p.out.loc[chain * d + r] = z0;
+        // row r of the identity: entries (r, j), j <= r
+        for (int j = 0; j <= r; ++j) Lout[col_off(d, j) + (r - j)] = (j == r) ? 1.0f : 0.0f;
+      }
+      if (r == 0) {
+        p.out.i[chain] = 0;
+        p.out.potential_energy[chain] = pe0;
+        p.out.mean_accept_prob[chain] = 0.0f;
+        p.out.log_step_size[chain] = 0.0f;
+        p.out.as_change[chain] = 0.0f;
+        p.out.rng_key[2 * chain] = kk.v[0];
+        p.out.rng_key[2 * chain + 1] = kk.v[1];
+      }
+    }
+  }
+}
+
+// --------------------------------------------------------- potential kernel --
+template <int DMAX, template <int> class M, bool EXACT>
+__global__ __launch_bounds__(kBlock) void potential_kernel(PotParams p) {
+  constexpr int G = DMAX;
+  using Gp = Grp<G>;
+  extern __shared__ float lds[];
+  const int d = EXACT ? DMAX : p.d;
+  M<G>::stage(lds, p.model, d);
+  __syncthreads();
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.n;
+  const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
+  const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t item = wave0; item < n_items; item += wstride) {
+    const int64_t chain = item_chain<G>(item);
+    const bool chain_ok = chain < C;
+    const int64_t cl = chain_ok ? chain : C - 1;
+    const float x = act ? p.z[cl * d + r] : 0.0f;
+    const float pe = M<G>::potential(x, r, d, p.model, lds);
+    if (chain_ok && r == 0) p.pe[chain] = pe;
+  }
+}
+
+// -------------------------------------------------------- sample_Pnx kernel --
+// arwmh.py:230-270: all chains share one frozen adapt state; chain c = (pt, s)
+// starts at x[pt] with key split(rng_key, C)[c] and runs n steps, noise at
+// stream position t.  L stays in registers for every chain the wave visits.
+template <int DMAX, template <int> class M, bool EXACT>
+__global__ __launch_bounds__(kBlock) void sample_pnx_kernel(PnxParams p) {
+  constexpr int G = DMAX;
+  using Gp = Grp<G>;
+  extern __shared__ float lds[];
+  const int d = EXACT ? DMAX : p.d;
+  M<G>::stage(lds, p.model, d);
+  __syncthreads();
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.n_points * p.n_samples;
+  const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
+  const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
+  float A[DMAX];
+#pragma unroll
+  for (int j = 0; j < DMAX; ++j) {
+    A[j] = 0.0f;
+    if (j < d) {
+      if (r >= j && act) A[j] = p.scale[col_off(d, j) + (r - j)];
+    }
+  }
+  const float el = amh_expf(p.log_step_size);
+  for (int64_t item = wave0; item < n_items; item += wstride) {
+    const int64_t chain = item_chain<G>(item);
+    const bool chain_ok = chain < C;
+    const int64_t cl = chain_ok ? chain : C - 1;
+    const int64_t pt = cl / p.n_samples;
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)cl, (uint32_t)((uint64_t)cl >> 32), 0u, AMH_TAG_SPLIT,
+                                           p.key0, p.key1);
+    float z = act ? p.x[pt * d + r] : 0.0f;
+    float pe = M<G>::potential(z, r, d, p.model, lds);
+    for (int32_t t = 0; t < p.n; ++t) {
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)t, 0u, AMH_TAG_STEP, kk.v[0], kk.v[1]);
+      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      float acc = 0.0f;
+      static_for<DMAX>([&](auto J) {
+        if (J < d) acc = fmaf(A[J], Gp::template bcast<J>(xi), acc);
+      });
+      const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+      float pep = M<G>::potential(zp, r, d, p.model, lds);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      const bool accept = u < alpha;
+      z = accept ? zp : z;
+      pe = accept ? pep : pe;
+    }
+    if (chain_ok && act) p.out[cl * d + r] = z;
+  }
+}
+
+// ------------------------------------------------------------ chain keys ----
+__global__ void chain_keys_kernel(uint32_t key0, uint32_t key1, int64_t offset, int64_t n, uint32_t* out) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const uint64_t g = (uint64_t)(offset + c);
+  const amh_u32x4 o = amh_philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), 0u, AMH_TAG_CHAINKEY, key0, key1);
+  out[2 * c] = o.v[0];
+  out[2 * c + 1] = o.v[1];
+}
+
+// ------------------------------------------------------------- launchers ----
+static int grid_for(int64_t n_items, int waves_per_block) {
+  // enough waves to cover 256 CUs x 8 waves/CU several times; grid-stride past it
+  const int64_t blocks = (n_items + waves_per_block - 1) / waves_per_block;
+  const int64_t cap = 256 * 32;
+  return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
+}
+
+template <int DMAX, template <int> class M, bool EXACT>
+hipError_t launch_step(const StepParams& p, hipStream_t s) {
+  const int64_t n_items = (p.C + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
+  const int64_t blocks = (n_items + kBlock / 64 - 1) / (kBlock / 64);  // one chain group per wave
+  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  hipLaunchKernelGGL((arwmh_step_kernel<DMAX, M, EXACT>), dim3((unsigned)blocks), dim3(kBlock), shm, s, p);
+  return hipGetLastError();
+}
+
+template <int DMAX, template <int> class M, bool EXACT>
+hipError_t launch_init(const InitParams& p, hipStream_t s) {
+  const int64_t n_items = (p.C + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
+  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  hipLaunchKernelGGL((arwmh_init_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
+                     shm, s, p);
+  return hipGetLastError();
+}
+
+template <int DMAX, template <int> class M, bool EXACT>
+hipError_t launch_pot(const PotParams& p, hipStream_t s) {
+  const int64_t n_items = (p.n + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
+  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  hipLaunchKernelGGL((potential_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
+                     shm, s, p);
+  return hipGetLastError();
+}
+
+template <int DMAX, template <int> class M, bool EXACT>
+hipError_t launch_pnx(const PnxParams& p, hipStream_t s) {
+  const int64_t n_items = (p.n_points * p.n_samples + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
+  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  hipLaunchKernelGGL((sample_pnx_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
+                     shm, s, p);
+  return hipGetLastError();
+}
+
+// Dispatch table over (model, d).  Instantiated shapes:
+//   Gaussian: exact d = 64 (headline), dynamic d <= 1,2,4,8,16,32,64
+//   eight schools: d <= 16;  kidiq: d = 4;  diamonds: d <= 32
+template <template <int> class M, class F>
+static hipError_t dispatch_dim(int d, bool allow_exact64, F&& f) {
+  if (d < 1 || d > 64) return hipErrorInvalidValue;
+  if (d == 64 && allow_exact64) return f.template operator()<64, M, true>();
+  if (d <= 1) return f.template operator()<1, M, false>();
+  if (d <= 2) return f.template operator()<2, M, false>();
+  if (d <= 4) return f.template operator()<4, M, false>();
+  if (d <= 8) return f.template operator()<8, M, false>();
+  if (d <= 16) return f.template operator()<16, M, false>();
+  if (d <= 32) return f.template operator()<32, M, false>();
+  return f.template operator()<64, M, false>();
+}
+
+template <class F>
+static hipError_t dispatch(int model_id, int d, F&& f) {
+  switch (model_id) {
+    case AMH_MODEL_GAUSSIAN:
+      return dispatch_dim<GaussianM>(d, true, f);
+    case AMH_MODEL_EIGHT_SCHOOLS:
+      if (d > 16) return hipErrorInvalidValue;
+      return f.template operator()<16, EightSchoolsM, false>();
+    case AMH_MODEL_KIDIQ:
+      if (d != 4) return hipErrorInvalidValue;
+      return f.template operator()<4, KidiqM, true>();
+    case AMH_MODEL_DIAMONDS:
+      if (d > 32) return hipErrorInvalidValue;
+      return f.template operator()<32, DiamondsM, false>();
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+struct StepF {
+  const StepParams& p;
+  hipStream_t s;
+  template <int D, template <int> class M, bool E>
+  hipError_t operator()() { return launch_step<D, M, E>(p, s); }
+};
+struct InitF {
+  const InitParams& p;
+  hipStream_t s;
+  template <int D, template <int> class M, bool E>
+  hipError_t operator()() { return launch_init<D, M, E>(p, s); }
+};
+struct PotF {
+  const PotParams& p;
+  hipStream_t s;
+  template <int D, template <int> class M, bool E>
+  hipError_t operator()() { return launch_pot<D, M, E>(p, s); }
+};
+struct PnxF {
+  const PnxParams& p;
+  hipStream_t s;
+  template <int D, template <int> class M, bool E>
+  hipError_t operator()() { return launch_pnx<D, M, E>(p, s); }
+};
+
+hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
+  return dispatch(model_id, p.d, StepF{p, s});
+}
+hipError_t run_init(int model_id, const InitParams& p, hipStream_t s) {
+  return dispatch(model_id, p.d, InitF{p, s});
+}
+hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s) {
+  return dispatch(model_id, p.d, PotF{p, s});
+}
+hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s) {
+  return dispatch(model_id, p.d, PnxF{p, s});
+}
+hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, uint32_t* out, hipStream_t s) {
+  const int blocks = (int)((n + 255) / 256);
+  hipLaunchKernelGGL(chain_keys_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, k0, k1, offset, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace amh

@@ -1,0 +1,9 @@
+"""Import surface of the reference (python/kernels/__init__.py:1):
+`from kernels import ARWMH, ARWMHState, ARWMHAdaptState`.
+
+ASSS / NUTS / SA are outside the accelerated path."""
+from .arwmh import ARWMH, ARWMHAdaptState, ARWMHState, init_to_uniform, pack_scale, packed_size, unpack_scale
+from .random import PRNGKey, split
+
+__all__ = ["ARWMH", "ARWMHState", "ARWMHAdaptState", "init_to_uniform", "pack_scale", "unpack_scale",
+           "packed_size", "PRNGKey", "split"]

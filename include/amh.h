@@ -1,0 +1,135 @@
+/*
+ * amh.h -- C ABI of libamh.so, the MI355X (gfx950) adaptive random-walk
+ * Metropolis-Hastings engine.
+ *
+ * The reference (savelovme/adaptive-mcmc) has no FFI: its boundary is the
+ * NumPyro MCMCKernel object python/kernels/arwmh.py:31.  Each entry point
+ * below replaces one method of that object for a whole batch of chains; the
+ * Python mirror (adaptive-mcmc_amd/kernels/arwmh.py) binds them with ctypes.
+ *
+ *   amh_create / amh_bind_model   ARWMH.__init__        arwmh.py:43-78
+ *                                 + model plug-in        arwmh.py:109-116
+ *   amh_init                      ARWMH.init            arwmh.py:84-138
+ *   amh_step                      ARWMH.sample          arwmh.py:140-207
+ *                                 (n_steps > 1: numpyro fori_collect over
+ *                                 sample, kernel_utils.py:29-33)
+ *   amh_potential                 potential_fn          arwmh.py:121,170
+ *   amh_sample_pnx                ARWMH.sample_Pnx      arwmh.py:230-270
+ *   amh_pooled_*                  build-defined pooled-covariance mode
+ *                                 (SURVEY.md §8(e)); no reference analogue
+ *
+ * Conventions
+ *   - Every pointer in amh_state / model data / outputs is a DEVICE pointer
+ *     owned by the caller (PyTorch allocates them).  The library never frees
+ *     caller memory.
+ *   - Layout is chain-major: z/loc [C][d], scale [C][d(d+1)/2] (lower
+ *     triangle packed column by column: column j holds rows j..d-1),
+ *     scalars [C], rng_key [C][2] uint32.
+ *   - All work is enqueued on `stream` (a hipStream_t; NULL = default
+ *     stream).  No call synchronises the device except amh_destroy.
+ *   - Return value: 0 on success, a negative AMH_E* code on failure;
+ *     amh_last_error(h) describes the failure (thread-local when h is NULL).
+ *   - One handle per device; handles are not shared between host threads.
+ */
+#ifndef AMH_H
+#define AMH_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AMH_ABI_VERSION 1
+
+enum {
+  AMH_OK = 0,
+  AMH_EINVAL = -1,   /* bad argument (shape, pointer, unsupported d)     */
+  AMH_ENOMODEL = -2, /* amh_step/amh_init before amh_bind_model          */
+  AMH_EHIP = -3,     /* HIP runtime error (message in amh_last_error)    */
+  AMH_ENOMEM = -4
+};
+
+/* Model plug-in registry (PosteriorDB models of the reference + Gaussian). */
+enum {
+  AMH_MODEL_GAUSSIAN = 1,      /* data: [m (d) | P (d*d) | c0]; U = .5 (x-m)'P(x-m) + c0   */
+  AMH_MODEL_EIGHT_SCHOOLS = 2, /* data: [y (J) | sigma (J) | log sigma (J)], d = J + 2     */
+  AMH_MODEL_KIDIQ = 3,         /* data: [kid (N) | mom_hs (N) | mom_iq (N)], d = 4          */
+  AMH_MODEL_DIAMONDS = 4       /* data: [Xc (N*Kc) | Y (N)], d = Kc + 2, Kc = K - 1        */
+};
+
+typedef struct amh_config {
+  int32_t dim;                /* d, flat unconstrained dimension (1..64)     */
+  int32_t num_warmup;         /* W (ARWMH.init's num_warmup)                 */
+  float lr_decay;             /* a: gamma_n = 1 / n^a          (default 2/3) */
+  float target_accept_prob;   /*                               (default .234)*/
+  float eps;                  /* eps added to the scaled factor (default 1e-6)*/
+  int32_t reserved[3];
+} amh_config;
+
+typedef struct amh_state {
+  int32_t* i;                 /* [C]      iteration                          */
+  float* z;                   /* [C][d]   current point (unconstrained)      */
+  float* potential_energy;    /* [C]                                          */
+  float* mean_accept_prob;    /* [C]                                          */
+  float* loc;                 /* [C][d]   adapt_state.loc                    */
+  float* scale;               /* [C][P]   adapt_state.scale, packed lower    */
+  float* log_step_size;       /* [C]      adapt_state.log_step_size          */
+  float* as_change;           /* [C]                                          */
+  uint32_t* rng_key;          /* [C][2]   per-chain Philox key               */
+} amh_state;
+
+/* Optional per-launch collection (numpyro fori_collect / extra_fields). */
+typedef struct amh_collect {
+  float* z;                   /* [n_keep][C][d] or NULL                      */
+  float* potential_energy;    /* [n_keep][C] or NULL                         */
+  int32_t* accept_count;      /* [C] incremented per accepted step, or NULL  */
+  int32_t thinning;           /* keep every `thinning`-th step (>= 1)        */
+} amh_collect;
+
+typedef struct amh_handle amh_handle;
+
+int amh_version(void);
+const char* amh_last_error(const amh_handle* h);
+
+/* arwmh.py:43-78 (constructor config). */
+int amh_create(const amh_config* cfg, int device, amh_handle** out);
+int amh_destroy(amh_handle* h);
+
+/* Model plug-in (arwmh.py:109-116 / the scripts' numpyro models).
+ * data: device pointer, n_data floats; iparams model-specific:
+ *   GAUSSIAN: none.  EIGHT_SCHOOLS: {J}.  KIDIQ: {N}.  DIAMONDS: {N, K}. */
+int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n_data,
+                   const int64_t* iparams, int32_t n_iparams);
+
+/* arwmh.py:84-138 for chains [chain_offset, chain_offset + C) of the run
+ * keyed by key[2] (host memory).  init_z: device [C][d] starting points, or
+ * NULL for init_to_uniform (U(-2, 2) per coordinate).  Writes *out. */
+int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t num_chains,
+             const float* init_z, const amh_state* out, void* stream);
+
+/* arwmh.py:140-207 applied n_steps times to every chain.  `in` and `out` may
+ * alias (in-place update).  collect may be NULL. */
+int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+             int32_t n_steps, const amh_collect* collect, void* stream);
+
+/* potential_fn(z) for n points: pe[n] from z[n][d] (arwmh.py:121). */
+int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* stream);
+
+/* arwmh.py:230-270.  x: device [n_points][d]; adapt state (loc[d],
+ * scale_packed[P], log_step_size) shared by every chain; out: device
+ * [n_points][n_samples][d].  key[2] in host memory. */
+int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t n_points,
+                   int64_t n_samples, const float* loc, const float* scale_packed,
+                   float log_step_size, int32_t n, float* out, void* stream);
+
+/* Per-chain key derivation used by amh_init (device out[n][2]); exposed so
+ * callers can reproduce chain streams. */
+int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint32_t* out,
+                   void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AMH_H */

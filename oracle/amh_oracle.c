@@ -1,0 +1,555 @@
+/*
+ * amh_oracle.c -- TEST INFRASTRUCTURE ONLY.  CPU restatement of the reference
+ * ARWMH hot path, used as the parity checker for the HIP kernels and as the
+ * `cpu_baseline` leg of bench.py.  Nothing in the product (the package under
+ * adaptive-mcmc_amd/) links, imports or calls this file.
+ *
+ * What it restates (reference = /root/reference, savelovme/adaptive-mcmc):
+ *   orc_init        arwmh.py:84-138   ARWMH.init (mu = z0, L = I, lambda = 0)
+ *                   + numpyro init_to_uniform: U(-2, 2) per unconstrained site
+ *   orc_step        arwmh.py:140-207  ARWMH.sample, one or more steps
+ *     cholupdate    numpyro.distributions.util.cholesky_update (called at
+ *                   arwmh.py:190; Krause & Igel 2015 rank-one update)
+ *   orc_sample_pnx  arwmh.py:230-270  ARWMH.sample_Pnx (frozen shared theta)
+ *   potentials      run_eight_schools_lr_decay.py:26-35,
+ *                   run_kidiq_kidscore_lr_decay.py:29-41,
+ *                   run_diamonds_lr_decay.py:24-40, and the build-defined
+ *                   dense Gaussian
+ *
+ * Arithmetic order follows the HIP kernel's (documented in DESIGN.md, "bit
+ * spec"), so GPU and oracle agree bit for bit; the order's faithfulness to
+ * the reference is pinned separately by tests/test_oracle.py against the
+ * literal numpy restatement oracle/arwmh_np.py (float64) within tolerance.
+ *
+ * Build: make -C oracle   (gcc -O2 -ffp-contract=off -fopenmp)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <math.h>
+#include "../include/amh_math.h"
+
+#define ORC_DMAX 64
+
+enum { ORC_GAUSSIAN = 1, ORC_EIGHT_SCHOOLS = 2, ORC_KIDIQ = 3, ORC_DIAMONDS = 4 };
+
+typedef struct {
+  int32_t model_id;
+  int32_t d;
+  int32_t num_warmup;
+  float lr_decay;
+  float target_accept_prob;
+  float eps;
+  const float* data;   /* model data, layout per model (see potential) */
+  int64_t n_data;      /* N rows for regression models                 */
+  int64_t k_data;      /* K columns for diamonds                       */
+} orc_cfg;
+
+/* Group (lane) width the GPU uses for dimension d: next power of two. */
+int orc_group_width(int d) {
+  int g = 1;
+  while (g < d) g <<= 1;
+  return g;
+}
+
+/* ----------------------------------------------------- lane-group ops ---- */
+/* butterfly sum: for off = 1,2,4,..: x[r] = x[r] + x[r ^ off] */
+static float group_sum(const float* in, int G) {
+  float x[ORC_DMAX], y[ORC_DMAX];
+  memcpy(x, in, sizeof(float) * G);
+  for (int off = 1; off < G; off <<= 1) {
+    for (int r = 0; r < G; ++r) y[r] = x[r] + x[r ^ off];
+    memcpy(x, y, sizeof(float) * G);
+  }
+  return x[0];
+}
+
+/* exclusive scan with the kernel's association (Grp::excl_scan): shift by one
+ * lane; inclusive Hillis-Steele inside 16-lane rows (DPP row_shr 1,2,4,8);
+ * then odd rows add lane 15 of the row before (row_bcast15) and, for G = 64,
+ * rows 2-3 add lane 31 (row_bcast31).  Each round reads the previous round's
+ * values (simultaneous update). */
+static void group_excl_scan(const float* t, float* out, int G) {
+  float x[ORC_DMAX], y[ORC_DMAX];
+  for (int r = 0; r < G; ++r) x[r] = (r >= 1) ? t[r - 1] : 0.0f;
+  for (int off = 1; off < 16 && off < G; off <<= 1) {
+    for (int r = 0; r < G; ++r) {
+      const int ok = (G >= 16) ? ((r % 16) >= off) : (r >= off);
+      y[r] = ok ? x[r] + x[r - off] : x[r];
+    }
+    memcpy(x, y, sizeof(float) * G);
+  }
+  if (G >= 32) {
+    for (int r = 0; r < G; ++r) y[r] = ((r / 16) % 2 == 1) ? x[r] + x[(r / 16) * 16 - 1] : x[r];
+    memcpy(x, y, sizeof(float) * G);
+  }
+  if (G == 64) {
+    for (int r = 0; r < G; ++r) y[r] = (r >= 32) ? x[r] + x[31] : x[r];
+    memcpy(x, y, sizeof(float) * G);
+  }
+  memcpy(out, x, sizeof(float) * G);
+}
+
+/* ------------------------------------------------------------- models ---- */
+#define HALF_LOG_2PI 0.918938533204672742f
+
+/* Dense Gaussian: data = [m (d) | P (d*d, symmetric precision) | c0].
+ * U(x) = 0.5 (x-m)' P (x-m) + c0. */
+static float pot_gaussian(const orc_cfg* cfg, const float* x, int G) {
+  const int d = cfg->d;
+  const float* m = cfg->data;
+  const float* P = cfg->data + d;
+  const float c0 = cfg->data[d + d * d];
+  float diff[ORC_DMAX], q[ORC_DMAX];
+  for (int r = 0; r < G; ++r) diff[r] = (r < d) ? x[r] - m[r] : 0.0f;
+  for (int r = 0; r < G; ++r) {
+    if (r >= d) { q[r] = 0.0f; continue; }
+    float y = 0.0f;
+    for (int j = 0; j < d; ++j) y = fmaf(P[r * d + j], diff[j], y); /* row r (LDS layout) */
+    q[r] = diff[r] * y;
+  }
+  const float S = group_sum(q, G);
+  return (0.5f * S) + c0;
+}
+
+/* Eight schools, non-centred (run_eight_schools_lr_decay.py:26-35).
+ * z = [mu, log tau, theta_base_0..J-1] (ravel_pytree sorted-key order).
+ * data = [y (J) | sigma (J) | log sigma (J)]. */
+static float pot_eight_schools(const orc_cfg* cfg, const float* x, int G) {
+  const int d = cfg->d, J = d - 2;
+  const float* y = cfg->data;
+  const float* sg = cfg->data + J;
+  const float* lsg = cfg->data + 2 * J;
+  const float mu = x[0], lt = x[1];
+  const float tau = amh_expf(lt);
+  float lp[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    float v = 0.0f;
+    if (r == 0) {
+      const float t = mu / 5.0f;
+      v = ((-0.5f * (t * t)) - 1.60943791243410037f) - HALF_LOG_2PI;
+    } else if (r == 1) {
+      const float t = tau / 5.0f;
+      /* log HalfCauchy(tau; 5) + log|d tau / d lt| */
+      v = ((-0.451582705289454865f - 1.60943791243410037f) - amh_log1pf(t * t)) + lt;
+    } else if (r < d) {
+      const int j = r - 2;
+      const float th = x[r];
+      const float lpt = (-0.5f * (th * th)) - HALF_LOG_2PI;
+      const float e = (y[j] - (mu + tau * th)) / sg[j];
+      const float lpy = ((-0.5f * (e * e)) - lsg[j]) - HALF_LOG_2PI;
+      v = lpt + lpy;
+    }
+    lp[r] = v;
+  }
+  return -group_sum(lp, G);
+}
+
+/* kidiq-kidscore_momhsiq (run_kidiq_kidscore_lr_decay.py:29-41).
+ * z = [beta0, beta1, beta2, log sigma]; data = [kid (N) | hs (N) | iq (N)].
+ * Lane r sums rows n = r, r+G, r+2G, ... */
+static float pot_kidiq(const orc_cfg* cfg, const float* x, int G) {
+  const int64_t N = cfg->n_data;
+  const float* kid = cfg->data;
+  const float* hs = cfg->data + N;
+  const float* iq = cfg->data + 2 * N;
+  const float b0 = x[0], b1 = x[1], b2 = x[2], ls = x[3];
+  const float sg = amh_expf(ls);
+  const float isg = 1.0f / sg;
+  float part[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      const float mu = fmaf(b2, iq[n], fmaf(b1, hs[n], b0));
+      const float e = (kid[n] - mu) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    part[r] = acc;
+  }
+  const float S = group_sum(part, G);
+  const float t = sg / 2.5f;
+  /* -[ N*(-log sigma - HALF_LOG_2PI) - S/2 + logHalfCauchy(sigma;2.5) + ls ] */
+  const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+  const float lpr = ((-0.451582705289454865f - 0.916290731874155065f) - amh_log1pf(t * t)) + ls;
+  return -(ll + lpr);
+}
+
+/* log StudentT(x; nu=3, loc, scale) up to the data-independent constant
+ * folded into c (= lgamma(2) - lgamma(1.5) - 0.5 log(3 pi) - log scale). */
+static float lp_student3(float x, float loc, float scale, float c) {
+  const float t = (x - loc) / scale;
+  return c - 2.0f * amh_log1pf((t * t) / 3.0f);
+}
+
+/* diamonds (run_diamonds_lr_decay.py:24-40).
+ * z = [Intercept, b_0..b_{K-2}, log sigma]; data = [Xc (N x Kc, row-major,
+ * centred) | Y (N)].  Lane r sums rows n = r, r+G, ... */
+static float pot_diamonds(const orc_cfg* cfg, const float* x, int G) {
+  const int64_t N = cfg->n_data;
+  const int Kc = (int)cfg->k_data - 1;
+  const float* X = cfg->data;
+  const float* Y = cfg->data + N * Kc;
+  const float icpt = x[0], ls = x[Kc + 1];
+  const float sg = amh_expf(ls);
+  const float isg = 1.0f / sg;
+  float part[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      float mu = 0.0f;
+      for (int k = 0; k < Kc; ++k) mu = fmaf(X[n * Kc + k], x[1 + k], mu);
+      const float e = (Y[n] - (icpt + mu)) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    part[r] = acc;
+  }
+  const float S = group_sum(part, G);
+  float bb[ORC_DMAX];
+  for (int r = 0; r < G; ++r) bb[r] = (r >= 1 && r <= Kc) ? x[r] * x[r] : 0.0f;
+  const float B = group_sum(bb, G);
+  const float cst = -3.30347394261755545f; /* lgamma(2)-lgamma(1.5)-.5log(3pi) - log 10 */
+  const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+  const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+  const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+  const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+  return -(((ll + lpb) + lpi) + lps);
+}
+
+float orc_potential1(const orc_cfg* cfg, const float* x) {
+  const int G = orc_group_width(cfg->d);
+  switch (cfg->model_id) {
+    case ORC_GAUSSIAN: return pot_gaussian(cfg, x, G);
+    case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
+    case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
+    case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
+    default: return NAN;
+  }
+}
+
+void orc_potential(const orc_cfg* cfg, const float* z, float* pe, int64_t n) {
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < n; ++c) pe[c] = orc_potential1(cfg, z + c * cfg->d);
+}
+
+/* ---------------------------------------------------------------- keys ---- */
+void orc_chain_keys(const uint32_t* key, int64_t chain_offset, int64_t n, uint32_t* out) {
+  for (int64_t c = 0; c < n; ++c) {
+    const uint64_t g = (uint64_t)(chain_offset + c);
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), 0u, AMH_TAG_CHAINKEY,
+                                          key[0], key[1]);
+    out[2 * c] = o.v[0];
+    out[2 * c + 1] = o.v[1];
+  }
+}
+
+/* ----------------------------------------------------------------- init ---- */
+static inline int64_t packed_size(int d) { return (int64_t)d * (d + 1) / 2; }
+static inline int64_t col_off(int d, int j) { return (int64_t)j * d - (int64_t)j * (j - 1) / 2; }
+
+void orc_init(const orc_cfg* cfg, const uint32_t* key, int64_t chain_offset, int64_t C,
+              const float* init_z, int32_t* i_, float* z, float* pe, float* macc, float* mu,
+              float* L, float* lam, float* asc, uint32_t* keys) {
+  const int d = cfg->d;
+  orc_chain_keys(key, chain_offset, C, keys);
+#pragma omp parallel for schedule(static)
+  for (int64_t c = 0; c < C; ++c) {
+    float* zc = z + c * d;
+    for (int r = 0; r < d; ++r) {
+      if (init_z) {
+        zc[r] = init_z[c * d + r];
+      } else {
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, 0u, 0u, AMH_TAG_INIT, keys[2 * c], keys[2 * c + 1]);
+        float v = (amh_unif01_from_bits(o.v[0]) * 4.0f) + (-2.0f);
+        zc[r] = (v < -2.0f) ? -2.0f : v;
+      }
+      mu[c * d + r] = zc[r];
+    }
+    pe[c] = orc_potential1(cfg, zc);
+    float* Lc = L + c * packed_size(d);
+    for (int64_t k = 0; k < packed_size(d); ++k) Lc[k] = 0.0f;
+    for (int j = 0; j < d; ++j) Lc[col_off(d, j)] = 1.0f;
+    i_[c] = 0;
+    macc[c] = 0.0f;
+    lam[c] = 0.0f;
+    asc[c] = 0.0f;
+  }
+}
+
+/* ----------------------------------------------------------------- step ---- */
+/* A chain between steps, as the kernel keeps it in registers: the factor in
+ * unit-lower form U (U_rr = 1, U_rj = L_rj / L_jj) plus its diagonal dl. */
+typedef struct {
+  int32_t i;
+  float pe, macc, lam, asc;
+  float z[ORC_DMAX], mu[ORC_DMAX], dl[ORC_DMAX];
+  float U[ORC_DMAX][ORC_DMAX];
+  int updated;
+} chain_t;
+
+/* One ARWMH transition of one chain (arwmh.py:140-207). Returns accept. */
+static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, uint32_t ctr) {
+  const int d = cfg->d;
+  const int G = orc_group_width(d);
+  /* arwmh.py:162-165: proposal noise and accept uniform */
+  float xi[ORC_DMAX];
+  uint32_t ubits = 0;
+  for (int r = 0; r < d; ++r) {
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, ctr, 0u, AMH_TAG_STEP, k0, k1);
+    xi[r] = amh_normal_from_bits(o.v[0]);
+    if (r == 0) ubits = o.v[1];
+  }
+  const float u = amh_unif01_from_bits(ubits);
+  /* arwmh.py:166-167: z' = z + (L e^lam + eps I) xi,  L xi = U (dl * xi) */
+  const float el = amh_expf(s->lam);
+  float eta[ORC_DMAX], zp[ORC_DMAX];
+  for (int r = 0; r < d; ++r) eta[r] = s->dl[r] * xi[r];
+  for (int r = 0; r < d; ++r) {
+    float acc = 0.0f;
+    for (int j = 0; j < d; ++j) acc = fmaf(s->U[r][j], eta[j], acc);
+    zp[r] = s->z[r] + fmaf(el, acc, cfg->eps * xi[r]);
+  }
+  /* arwmh.py:169-171 */
+  float pep = orc_potential1(cfg, zp);
+  if (amh_isnan(pep)) pep = INFINITY;
+  /* arwmh.py:173-178 */
+  const float ex = amh_expf(s->pe - pep);
+  const float alpha = (ex > 1.0f) ? 1.0f : ex;
+  const int acc = u < alpha;
+  float zn[ORC_DMAX];
+  for (int r = 0; r < d; ++r) zn[r] = acc ? zp[r] : s->z[r];
+  const float pen = acc ? pep : s->pe;
+  /* arwmh.py:180-185 */
+  const int32_t itr = s->i + 1;
+  const int32_t n = (s->i < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  const float maccn = s->macc + (alpha - s->macc) / (float)n;
+  /* arwmh.py:188-189 */
+  float delta[ORC_DMAX], mun[ORC_DMAX];
+  for (int r = 0; r < d; ++r) {
+    delta[r] = zn[r] - s->mu[r];
+    mun[r] = s->mu[r] + gamma * delta[r];
+  }
+  /* arwmh.py:193 */
+  const float lamn = s->lam + gamma * (alpha - cfg->target_accept_prob);
+  const float e1 = amh_expf(lamn);
+  /* arwmh.py:190-191: cholesky_update(sqrt(1-gamma) L, delta, gamma), NaN -> keep L */
+  const float sq = sqrtf(1.0f - gamma);
+  float Dg[ORC_DMAX], one[ORC_DMAX];
+  for (int j = 0; j < d; ++j) {
+    const float ajj = sq * s->dl[j];
+    Dg[j] = ajj * ajj;
+    one[j] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : NAN;
+  }
+  /* sweep 1: forward solve U w* = delta; w*_j captured when column j is applied */
+  float w[ORC_DMAX], ws[ORC_DMAX];
+  for (int r = 0; r < d; ++r) w[r] = delta[r];
+  for (int j = 0; j < d; ++j) {
+    const float wj = w[j];
+    ws[j] = wj;
+    for (int r = 0; r < d; ++r) w[r] = fmaf(-wj, s->U[r][j], w[r]);
+  }
+  /* per-column scalars, all columns at once; b_j by exclusive scan */
+  float t[ORC_DMAX], bsc[ORC_DMAX], cc[ORC_DMAX], qq[ORC_DMAX], gw2[ORC_DMAX], dnew[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    gw2[r] = (r < d) ? gamma * (ws[r] * ws[r]) : 0.0f;
+    t[r] = (r < d) ? gw2[r] / Dg[r] : 0.0f;
+  }
+  group_excl_scan(t, bsc, G);
+  int revert = 0;
+  for (int r = 0; r < d; ++r) {
+    const float b = 1.0f + bsc[r];
+    const float g = (b * Dg[r]) + gw2[r];
+    const float dn = g / b;
+    cc[r] = (gamma * ws[r]) / g;
+    qq[r] = sqrtf(dn);
+    dnew[r] = fmaf(cc[r], 0.0f, one[r]) * qq[r];
+    revert |= amh_isnan(dnew[r]);
+  }
+  float sacc[ORC_DMAX];
+  for (int r = 0; r < G; ++r) sacc[r] = 0.0f;
+  if (!revert) {
+    /* sweep 2: U'_rj = U_rj + c_j w_r^(j+1); as_change terms */
+    float ed[ORC_DMAX], qe[ORC_DMAX];
+    for (int r = 0; r < d; ++r) { ed[r] = s->dl[r] * el; qe[r] = qq[r] * e1; }
+    for (int r = 0; r < d; ++r) w[r] = delta[r];
+    for (int j = 0; j < d; ++j) {
+      for (int r = 0; r < d; ++r) {
+        const float uo = s->U[r][j];
+        w[r] = fmaf(-ws[j], uo, w[r]);
+        const float un = fmaf(cc[j], w[r], uo);
+        const float told = uo * ed[j];
+        const float tt = fmaf(un, qe[j], -told);
+        sacc[r] = fmaf(tt, tt, sacc[r]);
+        s->U[r][j] = un;
+      }
+    }
+    s->asc = sqrtf(group_sum(sacc, G));
+    for (int r = 0; r < d; ++r) s->dl[r] = qq[r];
+    s->updated = 1;
+  } else {
+    float ed0[ORC_DMAX], ed1[ORC_DMAX];
+    for (int r = 0; r < d; ++r) { ed0[r] = s->dl[r] * el; ed1[r] = s->dl[r] * e1; }
+    for (int j = 0; j < d; ++j)
+      for (int r = 0; r < d; ++r) {
+        const float uo = s->U[r][j];
+        const float told = uo * ed0[j];
+        const float tt = fmaf(uo, ed1[j], -told);
+        sacc[r] = fmaf(tt, tt, sacc[r]);
+      }
+    s->asc = sqrtf(group_sum(sacc, G));
+  }
+  s->i = itr;
+  for (int r = 0; r < d; ++r) { s->z[r] = zn[r]; s->mu[r] = mun[r]; }
+  s->pe = pen;
+  s->macc = maccn;
+  s->lam = lamn;
+  return acc;
+}
+
+/* launch-input conversion L -> (U, dl), kernel mirror */
+static void chain_load(const orc_cfg* cfg, chain_t* s, int64_t c, const int32_t* i_, const float* z,
+                       const float* pe, const float* macc, const float* mu, const float* L,
+                       const float* lam, const float* asc) {
+  const int d = cfg->d;
+  const float* Lc = L + c * packed_size(d);
+  float inv[ORC_DMAX];
+  for (int r = 0; r < d; ++r) {
+    s->dl[r] = Lc[col_off(d, r)];
+    inv[r] = (amh_isfinite(s->dl[r]) && s->dl[r] != 0.0f) ? 1.0f / s->dl[r] : 0.0f;
+  }
+  for (int r = 0; r < d; ++r)
+    for (int j = 0; j < d; ++j) {
+      const float x = (r > j) ? Lc[col_off(d, j) + (r - j)] : 0.0f;
+      s->U[r][j] = (r == j) ? 1.0f : x * inv[j];
+    }
+  for (int r = 0; r < d; ++r) { s->z[r] = z[c * d + r]; s->mu[r] = mu[c * d + r]; }
+  s->i = i_[c];
+  s->pe = pe[c];
+  s->macc = macc[c];
+  s->lam = lam[c];
+  s->asc = asc[c];
+  s->updated = 0;
+}
+
+/* L = U diag(dl) if any step of this launch updated the factor, else the
+ * launch-input factor verbatim (kernel mirror) */
+static void chain_store(const orc_cfg* cfg, const chain_t* s, int64_t c, const float* Lin, int32_t* i_,
+                        float* z, float* pe, float* macc, float* mu, float* L, float* lam, float* asc) {
+  const int d = cfg->d;
+  float* Lc = L + c * packed_size(d);
+  const float* L0 = Lin + c * packed_size(d);
+  for (int j = 0; j < d; ++j)
+    for (int r = j; r < d; ++r)
+      Lc[col_off(d, j) + (r - j)] = s->updated ? s->U[r][j] * s->dl[j] : L0[col_off(d, j) + (r - j)];
+  for (int r = 0; r < d; ++r) { z[c * d + r] = s->z[r]; mu[c * d + r] = s->mu[r]; }
+  i_[c] = s->i;
+  pe[c] = s->pe;
+  macc[c] = s->macc;
+  lam[c] = s->lam;
+  asc[c] = s->asc;
+}
+
+/* n_steps transitions of chains [0, C), in place (one kernel launch).  If
+ * collect_z is given it receives z after every step: collect_z[t][c][r].
+ * accept_count (nullable) is incremented per accepted proposal. */
+void orc_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe,
+              float* macc, float* mu, float* L, float* lam, float* asc, const uint32_t* keys,
+              int32_t* accept_count, float* collect_z) {
+  const int d = cfg->d;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t c = 0; c < C; ++c) {
+    chain_t* s = (chain_t*)malloc(sizeof(chain_t));
+    chain_load(cfg, s, c, i_, z, pe, macc, mu, L, lam, asc);
+    int nacc = 0;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      nacc += chain_step(cfg, s, keys[2 * c], keys[2 * c + 1], (uint32_t)s->i);
+      if (collect_z)
+        for (int r = 0; r < d; ++r) collect_z[((int64_t)t * C + c) * d + r] = s->z[r];
+    }
+    chain_store(cfg, s, c, L, i_, z, pe, macc, mu, L, lam, asc);
+    if (accept_count) accept_count[c] += nacc;
+    free(s);
+  }
+}
+
+/* ----------------------------------------------------------- sample_Pnx ---- */
+/* arwmh.py:230-270: every chain (p, s) starts at x[p] with key
+ * split(rng_key, (n_points, n_samples))[p, s] and runs n frozen-theta steps;
+ * only z (and pe) are carried.  Step t draws its noise at stream position t. */
+void orc_split_keys(const uint32_t* key, int64_t n, uint32_t* out) {
+  for (int64_t c = 0; c < n; ++c) {
+    const uint64_t g = (uint64_t)c;
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)g, (uint32_t)(g >> 32), 0u, AMH_TAG_SPLIT, key[0], key[1]);
+    out[2 * c] = o.v[0];
+    out[2 * c + 1] = o.v[1];
+  }
+}
+
+void orc_sample_pnx(const orc_cfg* cfg, const uint32_t* key, const float* x, int64_t n_points,
+                    int64_t n_samples, const float* loc, const float* Lpacked, float log_step_size,
+                    int32_t n, float* out) {
+  const int d = cfg->d;
+  const int64_t C = n_points * n_samples;
+  uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)C);
+  orc_split_keys(key, C, keys);
+  (void)loc;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t p = c / n_samples;
+    float A[ORC_DMAX][ORC_DMAX];
+    memset(A, 0, sizeof(A));
+    for (int j = 0; j < d; ++j)
+      for (int r = j; r < d; ++r) A[r][j] = Lpacked[col_off(d, j) + (r - j)];
+    float z[ORC_DMAX], zp[ORC_DMAX], xi[ORC_DMAX];
+    for (int r = 0; r < d; ++r) z[r] = x[p * d + r];
+    float pe = orc_potential1(cfg, z);
+    const float el = amh_expf(log_step_size);
+    for (int32_t t = 0; t < n; ++t) {
+      uint32_t ubits = 0;
+      for (int r = 0; r < d; ++r) {
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)t, 0u, AMH_TAG_STEP, keys[2 * c], keys[2 * c + 1]);
+        xi[r] = amh_normal_from_bits(o.v[0]);
+        if (r == 0) ubits = o.v[1];
+      }
+      const float u = amh_unif01_from_bits(ubits);
+      for (int r = 0; r < d; ++r) {
+        float acc = 0.0f;
+        for (int j = 0; j < d; ++j) acc = fmaf(A[r][j], xi[j], acc);
+        zp[r] = z[r] + fmaf(el, acc, cfg->eps * xi[r]);
+      }
+      float pep = orc_potential1(cfg, zp);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      if (u < alpha) {
+        for (int r = 0; r < d; ++r) z[r] = zp[r];
+        pe = pep;
+      }
+    }
+    for (int r = 0; r < d; ++r) out[c * d + r] = z[r];
+  }
+  free(keys);
+}
+
+/* ------------------------------------------- elementwise math (for tests) ---- */
+void orc_philox(const uint32_t* ctr, const uint32_t* key, uint32_t* out, int64_t n) {
+  for (int64_t i = 0; i < n; ++i) {
+    const amh_u32x4 o = amh_philox4x32_10(ctr[4 * i], ctr[4 * i + 1], ctr[4 * i + 2], ctr[4 * i + 3],
+                                          key[2 * i], key[2 * i + 1]);
+    memcpy(out + 4 * i, o.v, 16);
+  }
+}
+void orc_logf(const float* x, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_logf(x[i]); }
+void orc_expf(const float* x, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_expf(x[i]); }
+void orc_log1pf(const float* x, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_log1pf(x[i]); }
+void orc_erfinvf(const float* x, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_erfinvf(x[i]); }
+void orc_normal_bits(const uint32_t* b, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_normal_from_bits(b[i]); }
+void orc_lr_gamma(const int32_t* nn, float a, float* y, int64_t n) { for (int64_t i = 0; i < n; ++i) y[i] = amh_lr_gamma(nn[i], a); }
+int orc_num_threads(void) {
+#ifdef _OPENMP
+  extern int omp_get_max_threads(void);
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
