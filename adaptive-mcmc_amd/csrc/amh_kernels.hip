@@ -56,6 +56,14 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
+// Scheduling fence every K unrolled columns: the serial column sweeps have
+// little ILP to gain, and without fences the scheduler hoists independent
+// per-column products (64 of them) and runs out of VGPRs.
+template <int J, int K = 8>
+__device__ __forceinline__ void column_fence() {
+  if constexpr ((J % K) == K - 1) __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int CTRL, int ROWMASK = 0xF, bool BC = true>
 __device__ __forceinline__ float dppf(float old, float v) {
   return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWMASK, 0xF, BC));
@@ -171,7 +179,7 @@ struct GaussianM {
   // lane r reads its own row with ds_read_b128 (4 columns per read) and the
   // 16-B slots of the 16 lanes of a read group fall on distinct banks.
   static __host__ __device__ int ld(int d) { return ((d + 3) & ~3) + 4; }
-  static size_t lds_bytes(int d) { return (size_t)d * ld(d) * sizeof(float); }
+  static __host__ __device__ size_t lds_bytes(int d) { return (size_t)d * ld(d) * sizeof(float); }
   static __device__ void stage(float* lds, const ModelArgs& m, int d) {
     const float* P = m.data + d;
     const int L = ld(d);
@@ -210,7 +218,7 @@ struct GaussianM {
 template <int G>
 struct EightSchoolsM {
   // z = [mu, log tau, theta_base (J)]; data = [y (J) | sigma (J) | log sigma (J)]
-  static size_t lds_bytes(int) { return 0; }
+  static __host__ __device__ size_t lds_bytes(int) { return 0; }
   static __device__ void stage(float*, const ModelArgs&, int) {}
   static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
                                                     const float*) {
@@ -240,7 +248,7 @@ struct EightSchoolsM {
 template <int G>
 struct KidiqM {
   // z = [beta0, beta1, beta2, log sigma]; data = [kid | hs | iq] (N each)
-  static size_t lds_bytes(int) { return 0; }
+  static __host__ __device__ size_t lds_bytes(int) { return 0; }
   static __device__ void stage(float*, const ModelArgs&, int) {}
   static __device__ __forceinline__ float potential(float x, int r, int, const ModelArgs& m,
                                                     const float*) {
@@ -276,7 +284,7 @@ struct DiamondsM {
   // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)]
   // Straight VALU restatement (parity path); the MFMA GEMM path lives in
   // amh_diamonds.hip.
-  static size_t lds_bytes(int) { return 0; }
+  static __host__ __device__ size_t lds_bytes(int) { return 0; }
   static __device__ void stage(float*, const ModelArgs&, int) {}
   static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
                                                     const float*) {
@@ -314,7 +322,11 @@ struct DiamondsM {
 };
 
 // --------------------------------------------------------------- geometry --
-constexpr int kBlock = 256;  // 4 waves
+constexpr int kBlock = 256;       // 4 waves (init / potential / sample_Pnx kernels)
+constexpr int kBlockStep = 1024;  // 16 waves per CU share one staged copy of the model data
+#ifndef AMH_STEP_MIN_WAVES
+#define AMH_STEP_MIN_WAVES 1  // waves per SIMD the step kernel must fit (VGPR budget)
+#endif
 
 template <int G>
 struct Geo {
@@ -375,9 +387,128 @@ __device__ __forceinline__ float capture(float old, float v, int rr) {
   }
 }
 
+// ----------------------------------------------------------- lane masks --
+// Per-column lane predicates of the load/store phases.  For a full-wave
+// group they are compile-time lane masks built by one SALU shift inside the
+// asm (so the compiler can neither hoist 64 mask constants into SGPRs nor
+// keep them live across the chain loop); smaller groups compare an opaque
+// per-item copy of the lane index.
+template <int G, int J>
+__device__ __forceinline__ float keep_above(float x, int rr) {  // lanes r > J keep x, else 0
+  if constexpr (G == 64) {
+    if constexpr (J >= 63) {
+      return 0.0f;
+    } else {
+      float out;
+      unsigned long long m;
+      asm("s_lshl_b64 %1, -1, %3\n\tv_cndmask_b32_e64 %0, 0, %2, %1" : "=v"(out), "=&s"(m) : "v"(x), "n"(J + 1));
+      return out;
+    }
+  } else {
+    return (rr > J) ? x : 0.0f;
+  }
+}
+template <int G, int J>
+__device__ __forceinline__ float set_one_at(float x, int rr) {  // lane r == J gets 1.0
+  if constexpr (G == 64) {
+    float out;
+    unsigned long long m;
+    asm("s_lshl_b64 %1, 1, %3\n\tv_cndmask_b32_e64 %0, %2, 1.0, %1" : "=v"(out), "=&s"(m) : "v"(x), "n"(J));
+    return out;
+  } else {
+    return (rr == J) ? 1.0f : x;
+  }
+}
+template <int G, int J>
+__device__ __forceinline__ uint32_t off_from(uint32_t v, uint32_t oob, int rr) {  // lanes r >= J keep v, else oob
+  if constexpr (G == 64) {
+    uint32_t out;
+    unsigned long long m;
+    asm("s_lshl_b64 %1, -1, %4\n\tv_cndmask_b32_e64 %0, %3, %2, %1" : "=v"(out), "=&s"(m) : "v"(v), "v"(oob), "n"(J));
+    return out;
+  } else {
+    return (rr >= J) ? v : oob;
+  }
+}
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef __attribute__((address_space(3))) float lds_float;
+__device__ __forceinline__ lds_void* to_lds(const float* p) { return (lds_void*)(p); }
+
+// Per-wave LDS staging buffer of the step kernel, in floats:
+//   [ L: CPW*P (rounded to 4) | z: CPW*d | loc: CPW*d | scalars: 8 x CPW ]
+__host__ __device__ __forceinline__ int wbuf_L(int cpw, int d) { return ((cpw * d * (d + 1) / 2) + 3) & ~3; }
+__host__ __device__ __forceinline__ int wbuf_zd(int cpw, int d) { return ((cpw * d) + 3) & ~3; }
+__host__ __device__ __forceinline__ int wbuf_floats(int cpw, int d) {
+  return wbuf_L(cpw, d) + 2 * wbuf_zd(cpw, d) + 8 * cpw;
+}
+
+// Issue the DMA of one work item's chain state (global -> this wave's LDS
+// buffer).  Out-of-range bytes (past C) read as zero.
+template <int G>
+__device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first, int d, float* wb, int lane) {
+  constexpr int CPW = Geo<G>::CPW;
+  const uint32_t P = (uint32_t)(d * (d + 1) / 2);
+  const int64_t nvalid = (p.C - first) < CPW ? (p.C - first) : CPW;  // chains of this item in range
+  float* wL = wb;
+  float* wz = wb + wbuf_L(CPW, d);
+  float* wm = wz + wbuf_zd(CPW, d);
+  float* ws = wm + wbuf_zd(CPW, d);
+  {
+    const uint32_t bytes = (uint32_t)nvalid * P * 4u;
+    const Buf b(uniform_ptr(p.in.scale + first * P), bytes);
+    const bool vec = ((P * 4u) % 16u) == 0u;  // 16-B aligned chain blocks
+    const uint32_t total = (uint32_t)CPW * P * 4u;
+    // whole 1 KB pieces as dwordx4, the tail as dwords; exec masks keep every
+    // DMA inside this wave's buffer (an LDS-DMA writes base + 4*size*lane)
+    const uint32_t n16 = vec ? (total / 1024u) * 1024u : 0u;
+    for (uint32_t o = 0; o < n16; o += 1024u)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 16, (int)(o + 16u * lane), 0, 0, 0);
+    for (uint32_t o = n16; o < total; o += 256u) {
+      if (o + 4u * lane < total)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 4, (int)(o + 4u * lane), 0, 0, 0);
+    }
+  }
+  {
+    const uint32_t bytes = (uint32_t)(nvalid * d) * 4u;
+    const uint32_t total = (uint32_t)(CPW * d) * 4u;
+    const Buf bz(uniform_ptr(p.in.z + first * d), bytes);
+    const Buf bm(uniform_ptr(p.in.loc + first * d), bytes);
+    for (uint32_t o = 0; o < total; o += 256u) {
+      if (o + 4u * lane < total) {
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bz.rs, to_lds(wz + o / 4u), 4, (int)(o + 4u * lane), 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bm.rs, to_lds(wm + o / 4u), 4, (int)(o + 4u * lane), 0, 0, 0);
+      }
+    }
+  }
+  if (lane < CPW) {
+    const uint32_t bytes = (uint32_t)nvalid * 4u;
+    const uint32_t vo = 4u * lane;
+    const Buf b0(uniform_ptr(p.in.i + first), bytes);
+    const Buf b1(uniform_ptr(p.in.potential_energy + first), bytes);
+    const Buf b2(uniform_ptr(p.in.mean_accept_prob + first), bytes);
+    const Buf b3(uniform_ptr(p.in.log_step_size + first), bytes);
+    const Buf b4(uniform_ptr(p.in.as_change + first), bytes);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b0.rs, to_lds(ws + 0 * CPW), 4, (int)vo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b1.rs, to_lds(ws + 1 * CPW), 4, (int)vo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b2.rs, to_lds(ws + 2 * CPW), 4, (int)vo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b3.rs, to_lds(ws + 3 * CPW), 4, (int)vo, 0, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(b4.rs, to_lds(ws + 4 * CPW), 4, (int)vo, 0, 0, 0);
+  }
+  if (lane < 2 * CPW) {
+    const Buf bk(uniform_ptr(p.in.rng_key + 2 * first), (uint32_t)nvalid * 8u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(bk.rs, to_lds(ws + 5 * CPW), 4, (int)(4u * lane), 0, 0, 0);
+  }
+}
+
 // -------------------------------------------------------------- step kernel --
 // One or more ARWMH transitions (arwmh.py:140-207) per chain with the state
 // held in registers between steps.
+//
+// Persistent waves walk the chain groups; while a wave computes one group
+// (state in registers) the DMA engine streams the next group's state from HBM
+// into the wave's LDS buffer (buffer_load ... lds), so the HBM traffic of
+// the state round trip overlaps the arithmetic.
 //
 // Between steps the factor lives in registers in unit-lower form: U[j] holds
 // U_rj = L_rj / L_jj (U_rr = 1 exactly, zero above the diagonal) and `dl`
@@ -387,7 +518,7 @@ __device__ __forceinline__ float capture(float old, float v, int rr) {
 // column passes (w - w*1), which keeps the upper triangle at exact zeros.
 // L = U diag(dl) is formed only when the state is written back.
 template <int DMAX, template <int> class M, bool EXACT>
-__global__ __launch_bounds__(kBlock) void arwmh_step_kernel(StepParams p) {
+__global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   constexpr int G = DMAX;
   constexpr int CPW = Geo<G>::CPW;
   using Gp = Grp<G>;
@@ -396,225 +527,272 @@ __global__ __launch_bounds__(kBlock) void arwmh_step_kernel(StepParams p) {
   M<G>::stage(lds, p.model, d);
   __syncthreads();
 
-  const int r = Gp::r();
-  const bool act = r < d;
   const int64_t C = p.C;
   const uint32_t P = (uint32_t)(d * (d + 1) / 2);
-  const int64_t item = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
-  const int64_t first = (int64_t)__builtin_amdgcn_readfirstlane((int)(item * CPW));
-  if (first >= C) return;  // whole wave past the end (wave-uniform)
-  const int64_t chain = first + lane_id() / G;
-  const bool chain_ok = chain < C;
-  const int64_t cl = chain_ok ? chain : C - 1;
-  const uint32_t gsub = (uint32_t)(cl - first);  // group's chain within the wave block
+  const int64_t n_items = (C + CPW - 1) / CPW;
+  const int64_t wave = (int64_t)blockIdx.x * (kBlockStep / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlockStep / 64);
+  const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));  // wave-uniform
+  float* wb = lds + ((M<G>::lds_bytes(d) / sizeof(float) + 3) & ~(size_t)3) +
+              (size_t)wave_in_block * wbuf_floats(CPW, d);
+  const float* wL = wb;
+  const float* wz = wb + wbuf_L(CPW, d);
+  const float* wm = wz + wbuf_zd(CPW, d);
+  const float* wsc = wm + wbuf_zd(CPW, d);
+  const uint32_t oob = kOOB;
 
-  // wave block of the packed factors, in and out
-  const uint32_t wave_bytes = (uint32_t)CPW * P * 4u;
-  const Buf Lin(uniform_ptr(p.in.scale + first * P), wave_bytes);
-  const Buf Lout(uniform_ptr(p.out.scale + first * P), wave_bytes);
-  const uint32_t vrow = (gsub * P + (uint32_t)r) * 4u;  // lane's row offset (column 0)
-
-  // ---- load state
+  // Registers carry one chain group at a time.  Iteration k: wait for the
+  // DMA of item k, write item k-1 back (its registers are still live), read
+  // item k from LDS, start the DMA of item k+1, compute item k.  Stores are
+  // issued after the wait, so the next wait never has to drain them.
   float U[DMAX];
-  float dl, inv;
-  {
-    const uint32_t dofs = act ? (gsub * P + (uint32_t)col_off(d, r)) * 4u : kOOB;
-    dl = Lin.ld(dofs, 0);
-    inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+  float dl = 0.0f, z = 0.0f, mu = 0.0f, pe = 0.0f, macc = 0.0f, lam = 0.0f, asc = 0.0f;
+  int32_t it = 0, nacc = 0;
+  uint32_t k0 = 0, k1 = 0;
+  bool updated = false;
+  int64_t prev = -1;  // item whose state the registers hold
+  static_for<DMAX>([&](auto J) { U[J] = 0.0f; });
+
+  // write the registers' chain group (item `it_item`) back to HBM
+  auto store_item = [&](int64_t it_item, int lane) {
+    const int r = lane & (G - 1);
+    const int rr = r;
+    const bool act = r < d;
+    const int g = lane / G;
+    const int64_t first = it_item * CPW;
+    const int64_t chain = first + g;
+    const bool chain_ok = chain < C;
+    // L = U diag(dl); factors no step of this launch updated are copied from
+    // the launch input verbatim
+    const bool any_upd = Gp::any(updated);
+    const uint32_t vrow = (act && chain_ok) ? ((uint32_t)g * P + (uint32_t)r) * 4u : kOOB;
+    const uint32_t wave_bytes = (uint32_t)CPW * P * 4u;
+    const Buf Lout(uniform_ptr(p.out.scale + first * P), wave_bytes);
+    const Buf Lin(uniform_ptr(p.in.scale + first * P), wave_bytes);
     static_for<DMAX>([&](auto J) {
       constexpr int j = J;
-      U[j] = 0.0f;
       if (j < d) {
         const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
-        const float x = Lin.ld((r > j && act) ? vrow : kOOB, so);
-        const float ij = Gp::template bcast<j>(inv);
-        U[j] = (r == j) ? 1.0f : x * ij;
+        const uint32_t vo = off_from<G, j>(vrow, oob, rr);
+        float v;
+        if (any_upd) {
+          v = U[j] * Gp::template bcast<j>(dl);
+        } else {
+          v = Lin.ld(vo, so);
+        }
+        Lout.st(v, vo, so);
       }
+      column_fence<j>();
     });
-  }
-  float z = act ? p.in.z[cl * d + r] : 0.0f;
-  float mu = act ? p.in.loc[cl * d + r] : 0.0f;
-  int32_t it = p.in.i[cl];
-  float pe = p.in.potential_energy[cl];
-  float macc = p.in.mean_accept_prob[cl];
-  float lam = p.in.log_step_size[cl];
-  float asc = p.in.as_change[cl];
-  const uint32_t k0 = p.in.rng_key[2 * cl], k1 = p.in.rng_key[2 * cl + 1];
-  int32_t nacc = 0;
-  bool updated = false;
-
-  for (int32_t t = 0; t < p.n_steps; ++t) {
-    int rr = r;
-    if constexpr (G < 64) asm volatile("" : "+v"(rr));  // keep per-column compares in the loop
-
-    // ---- noise (arwmh.py:162-165, 174): stream position = state.i
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-    const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
-    const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
-
-    // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
-    //      L xi = U (dl * xi)
-    const float el = amh_expf(lam);
-    const float eta = dl * xi;
-    float acc = 0.0f;
-    static_for<DMAX>([&](auto J) {
-      if (J < d) acc = fmaf(U[J], Gp::template bcast<J>(eta), acc);
-    });
-    const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
-
-    // ---- potential, NaN -> +inf (arwmh.py:169-171)
-    float pep = M<G>::potential(zp, r, d, p.model, lds);
-    if (amh_isnan(pep)) pep = INFINITY;
-
-    // ---- accept / reject (arwmh.py:173-178)
-    const float ex = amh_expf(pe - pep);
-    const float alpha = (ex > 1.0f) ? 1.0f : ex;
-    const bool accept = u < alpha;
-    const float zn = accept ? zp : z;
-    const float pen = accept ? pep : pe;
-    nacc += accept ? 1 : 0;
-
-    // ---- schedule (arwmh.py:180-185)
-    const int32_t itr = it + 1;
-    const int32_t n = (it < p.W) ? itr : itr - p.W;
-    const float gamma = (n < p.gamma_tab_n) ? p.gamma_tab[n] : lr_gamma_slow(n, p.a);
-    const float maccn = macc + (alpha - macc) / (float)n;
-
-    // ---- mean and step size (arwmh.py:188-189, 193)
-    const float delta = act ? zn - mu : 0.0f;
-    const float mun = act ? mu + gamma * delta : 0.0f;
-    const float lamn = lam + gamma * (alpha - p.target);
-    const float e1 = amh_expf(lamn);
-
-    // ---- rank-one update of sqrt(1-gamma) L by (delta, gamma)
-    //      (arwmh.py:190-191 -> numpyro cholesky_update), NaN -> keep L.
-    const float sq = sqrtf(1.0f - gamma);
-    const float ajj = sq * dl;
-    const float Dg = ajj * ajj;
-    const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
-
-    // sweep 1: w*_j = w_j when column j is applied (forward solve U w* = delta)
-    float w = delta;
-    float ws = 0.0f;
-    static_for<DMAX>([&](auto J) {
-      if (J < d) {
-        const float wj = Gp::template bcast<J>(w);
-        ws = capture<G, J>(ws, wj, rr);
-        w = fmaf(-wj, U[J], w);
+    if (chain_ok) {
+      if (act) {
+        p.out.z[chain * d + r] = z;
+        p.out.loc[chain * d + r] = mu;
       }
-    });
+      if (r == 0) {
+        p.out.i[chain] = it;
+        p.out.potential_energy[chain] = pe;
+        p.out.mean_accept_prob[chain] = macc;
+        p.out.log_step_size[chain] = lam;
+        p.out.as_change[chain] = asc;
+        p.out.rng_key[2 * chain] = k0;
+        p.out.rng_key[2 * chain + 1] = k1;
+        if (p.accept_count != nullptr) p.accept_count[chain] += nacc;
+      }
+    }
+  };
 
-    // per-column scalars, one column per lane; b_j by exclusive scan
-    const float gw2 = act ? gamma * (ws * ws) : 0.0f;
-    const float tsc = act ? gw2 / Dg : 0.0f;
-    const float b = 1.0f + Gp::excl_scan(tsc, rr);
-    const float g = (b * Dg) + gw2;
-    const float dn = g / b;
-    const float c = (gamma * ws) / g;
-    const float q = sqrtf(dn);
-    const float dnew = fmaf(c, 0.0f, one) * q;  // new diagonal of column r
+  int64_t item = wave;
+  if (item < n_items) prefetch_item<G>(p, item * CPW, d, wb, lane_id());
 
-    const bool revert = Gp::any(act && amh_isnan(dnew));
-    // A NaN anywhere in numpyro's updated factor shows up in its new diagonal
-    // (fmaf(c, 0, U_jj) q_j): c_j, q_j and U_jj = A_jj / A_jj are the only
-    // per-column quantities, and every off-diagonal entry is finite whenever
-    // they are ("keep-L rule").  So the keep-L test of
-    // arwmh.py:191 is decided before the factor is touched.
-    float sacc = 0.0f;
-    if (!revert) {
-      // sweep 2: U'_rj = U_rj + c_j w_r^{(j+1)};  as_change terms
-      //   L'_rj e1 - L_rj e0 = U'_rj (q_j e1) - U_rj (dl_j e0)
-      const float ed = dl * el;
-      const float qe = q * e1;
-      w = delta;
+  for (; item < n_items; item += wstride) {
+    // Every lane-dependent quantity is derived from an opaque copy of the lane
+    // id inside the loop: otherwise the compiler hoists dozens of per-column
+    // addresses and masks out of this persistent loop and runs out of VGPRs.
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int r = lane & (G - 1);
+    const int rr = r;
+    const bool act = r < d;
+    const int64_t first = item * CPW;
+    const int g = lane / G;
+    const int64_t chain = first + g;
+    const bool chain_ok = chain < C;
+
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this item's DMA has landed
+    if (prev >= 0) store_item(prev, lane);
+
+    // ---- state: LDS -> registers
+    {
+      // LDS addresses made opaque per item so the 64 column addresses are
+      // not hoisted out of the chain loop (one base VGPR + immediate offsets)
+      lds_float* Lrow = (lds_float*)(wL + g * P + r);
+      asm volatile("" : "+v"(Lrow));
+      const lds_float* Lg = (const lds_float*)(wL + g * P);
+      dl = act ? Lg[col_off(d, r)] : 0.0f;
+      const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+      static_for<DMAX>([&](auto J) {
+        constexpr int j = J;
+        U[j] = 0.0f;
+        if (j < d) {
+          const float x = Lrow[col_off(d, j) - j];  // garbage for r < j: masked below
+          U[j] = set_one_at<G, j>(keep_above<G, j>(x * Gp::template bcast<j>(inv), rr), rr);
+        }
+        column_fence<j>();
+      });
+      z = act ? wz[g * d + r] : 0.0f;
+      mu = act ? wm[g * d + r] : 0.0f;
+      it = __float_as_int(wsc[0 * CPW + g]);
+      pe = wsc[1 * CPW + g];
+      macc = wsc[2 * CPW + g];
+      lam = wsc[3 * CPW + g];
+      asc = wsc[4 * CPW + g];
+      k0 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g]);
+      k1 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g + 1]);
+    }
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): buffer consumed before it is refilled
+    if (item + wstride < n_items) prefetch_item<G>(p, (item + wstride) * CPW, d, wb, lane);
+
+    nacc = 0;
+    updated = false;
+    for (int32_t t = 0; t < p.n_steps; ++t) {
+      // ---- noise (arwmh.py:162-165, 174): stream position = state.i
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+
+      // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
+      //      L xi = U (dl * xi)
+      const float el = amh_expf(lam);
+      const float eta = dl * xi;
+      float acc = 0.0f;
+      static_for<DMAX>([&](auto J) {
+        if (J < d) acc = fmaf(U[J], Gp::template bcast<J>(eta), acc);
+        column_fence<J, 16>();
+      });
+      const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+
+      // ---- potential, NaN -> +inf (arwmh.py:169-171)
+      float pep = M<G>::potential(zp, r, d, p.model, lds);
+      if (amh_isnan(pep)) pep = INFINITY;
+
+      // ---- accept / reject (arwmh.py:173-178)
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      const bool accept = u < alpha;
+      const float zn = accept ? zp : z;
+      const float pen = accept ? pep : pe;
+      nacc += accept ? 1 : 0;
+
+      // ---- schedule (arwmh.py:180-185)
+      const int32_t itr = it + 1;
+      const int32_t n = (it < p.W) ? itr : itr - p.W;
+      const float gamma = (n < p.gamma_tab_n) ? p.gamma_tab[n] : lr_gamma_slow(n, p.a);
+      const float maccn = macc + (alpha - macc) / (float)n;
+
+      // ---- mean and step size (arwmh.py:188-189, 193)
+      const float delta = act ? zn - mu : 0.0f;
+      const float mun = act ? mu + gamma * delta : 0.0f;
+      const float lamn = lam + gamma * (alpha - p.target);
+      const float e1 = amh_expf(lamn);
+
+      // ---- rank-one update of sqrt(1-gamma) L by (delta, gamma)
+      //      (arwmh.py:190-191 -> numpyro cholesky_update), NaN -> keep L.
+      const float sq = sqrtf(1.0f - gamma);
+      const float ajj = sq * dl;
+      const float Dg = ajj * ajj;
+      const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+
+      // sweep 1: w*_j = w_j when column j is applied (forward solve U w* = delta)
+      float w = delta;
+      float ws = 0.0f;
       static_for<DMAX>([&](auto J) {
         if (J < d) {
-          const float wj = Gp::template bcast<J>(ws);
-          const float cj = Gp::template bcast<J>(c);
-          const float edj = Gp::template bcast<J>(ed);
-          const float qej = Gp::template bcast<J>(qe);
-          const float uo = U[J];
-          w = fmaf(-wj, uo, w);
-          const float un = fmaf(cj, w, uo);
-          const float told = uo * edj;
-          const float tt = fmaf(un, qej, -told);
-          sacc = fmaf(tt, tt, sacc);
-          U[J] = un;
+          const float wj = Gp::template bcast<J>(w);
+          ws = capture<G, J>(ws, wj, rr);
+          w = fmaf(-wj, U[J], w);
         }
+        column_fence<J>();
       });
-      asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
-      dl = act ? q : 0.0f;
-      updated = true;
-    }
-    if (revert) {
-      // factor unchanged: as_change = || L (e1 - e0) ||_F
-      const float ed0 = dl * el;
-      const float ed1 = dl * e1;
-      sacc = 0.0f;
-      static_for<DMAX>([&](auto J) {
-        if (J < d) {
-          const float uo = U[J];
-          const float told = uo * Gp::template bcast<J>(ed0);
-          const float tt = fmaf(uo, Gp::template bcast<J>(ed1), -told);
-          sacc = fmaf(tt, tt, sacc);
-        }
-      });
-      asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
-    }
 
-    // ---- commit (arwmh.py:199-207)
-    it = itr;
-    z = zn;
-    pe = pen;
-    macc = maccn;
-    mu = mun;
-    lam = lamn;
+      // per-column scalars, one column per lane; b_j by exclusive scan
+      const float gw2 = act ? gamma * (ws * ws) : 0.0f;
+      const float tsc = act ? gw2 / Dg : 0.0f;
+      const float b = 1.0f + Gp::excl_scan(tsc, rr);
+      const float g2 = (b * Dg) + gw2;
+      const float dn = g2 / b;
+      const float c = (gamma * ws) / g2;
+      const float q = sqrtf(dn);
+      const float dnew = fmaf(c, 0.0f, one) * q;  // new diagonal of column r
 
-    if (p.col_z != nullptr || p.col_pe != nullptr) {
-      if ((t + 1) % p.thinning == 0 && chain_ok) {
-        const int64_t k = t / p.thinning;
-        if (p.col_z != nullptr && act) p.col_z[(k * C + chain) * d + r] = z;
-        if (p.col_pe != nullptr && r == 0) p.col_pe[k * C + chain] = pe;
-      }
-    }
-  }
-
-  // ---- store state: L = U diag(dl); untouched factors are copied verbatim
-  const bool any_upd = Gp::any(updated);
-  int r3 = r;
-  asm volatile("" : "+v"(r3));
-  uint32_t vrow3 = vrow;
-  asm volatile("" : "+v"(vrow3));
-  const bool st_ok = (r3 < d) && chain_ok;
-  static_for<DMAX>([&](auto J) {
-    constexpr int j = J;
-    if (j < d) {
-      const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
-      const uint32_t vo = (r3 >= j && st_ok) ? vrow3 : kOOB;
-      float v;
-      if (any_upd) {
-        v = U[j] * Gp::template bcast<j>(dl);
+      // A NaN anywhere in numpyro's updated factor shows up in its new diagonal
+      // (fmaf(c, 0, U_jj) q_j): c_j, q_j and U_jj = A_jj / A_jj are the only
+      // per-column quantities, and every off-diagonal entry is finite whenever
+      // they are ("keep-L rule").  So the keep-L test of
+      // arwmh.py:191 is decided before the factor is touched.
+      const bool revert = Gp::any(act && amh_isnan(dnew));
+      float sacc = 0.0f;
+      if (!revert) {
+        // sweep 2: U'_rj = U_rj + c_j w_r^{(j+1)};  as_change terms
+        //   L'_rj e1 - L_rj e0 = U'_rj (q_j e1) - U_rj (dl_j e0)
+        //   = U_rj (q_j e1 - dl_j e0) + (c_j q_j e1) w_r^{(j+1)}
+        const float ac = (q * e1) - (dl * el);
+        const float bc = (c * q) * e1;
+        w = delta;
+        static_for<DMAX>([&](auto J) {
+          if (J < d) {
+            const float wj = Gp::template bcast<J>(ws);
+            const float cj = Gp::template bcast<J>(c);
+            const float aj = Gp::template bcast<J>(ac);
+            const float bj = Gp::template bcast<J>(bc);
+            const float uo = U[J];
+            w = fmaf(-wj, uo, w);
+            const float un = fmaf(cj, w, uo);
+            const float tt = fmaf(uo, aj, bj * w);
+            sacc = fmaf(tt, tt, sacc);
+            U[J] = un;
+          }
+          column_fence<J>();
+        });
+        asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
+        dl = act ? q : 0.0f;
+        updated = true;
       } else {
-        v = Lin.ld(vo, so);
+        // factor unchanged: as_change = || L (e1 - e0) ||_F, L_rj = U_rj dl_j
+        const float ac = (dl * e1) - (dl * el);
+        static_for<DMAX>([&](auto J) {
+          if (J < d) {
+            const float tt = U[J] * Gp::template bcast<J>(ac);
+            sacc = fmaf(tt, tt, sacc);
+          }
+          column_fence<J>();
+        });
+        asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
       }
-      Lout.st(v, vo, so);
+
+      // ---- commit (arwmh.py:199-207)
+      it = itr;
+      z = zn;
+      pe = pen;
+      macc = maccn;
+      mu = mun;
+      lam = lamn;
+
+      if (p.col_z != nullptr || p.col_pe != nullptr) {
+        if ((t + 1) % p.thinning == 0 && chain_ok) {
+          const int64_t k = t / p.thinning;
+          if (p.col_z != nullptr && act) p.col_z[(k * C + chain) * d + r] = z;
+          if (p.col_pe != nullptr && r == 0) p.col_pe[k * C + chain] = pe;
+        }
+      }
     }
-  });
-  if (chain_ok) {
-    if (act) {
-      p.out.z[chain * d + r] = z;
-      p.out.loc[chain * d + r] = mu;
-    }
-    if (r == 0) {
-      p.out.i[chain] = it;
-      p.out.potential_energy[chain] = pe;
-      p.out.mean_accept_prob[chain] = macc;
-      p.out.log_step_size[chain] = lam;
-      p.out.as_change[chain] = asc;
-      p.out.rng_key[2 * chain] = k0;
-      p.out.rng_key[2 * chain + 1] = k1;
-      if (p.accept_count != nullptr) p.accept_count[chain] += nacc;
-    }
+
+    prev = item;
+  }
+  if (prev >= 0) {
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    store_item(prev, lane);
   }
 }
 
@@ -776,10 +954,28 @@ static int grid_for(int64_t n_items, int waves_per_block) {
 
 template <int DMAX, template <int> class M, bool EXACT>
 hipError_t launch_step(const StepParams& p, hipStream_t s) {
-  const int64_t n_items = (p.C + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
-  const int64_t blocks = (n_items + kBlock / 64 - 1) / (kBlock / 64);  // one chain group per wave
-  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
-  hipLaunchKernelGGL((arwmh_step_kernel<DMAX, M, EXACT>), dim3((unsigned)blocks), dim3(kBlock), shm, s, p);
+  constexpr int CPW = Geo<DMAX>::CPW;
+  constexpr int WPB = kBlockStep / 64;
+  const int d = EXACT ? DMAX : p.d;
+  const int64_t n_items = (p.C + CPW - 1) / CPW;
+  const size_t model_floats = (M<DMAX>::lds_bytes(d) / sizeof(float) + 3) & ~(size_t)3;
+  const size_t shm = (model_floats + (size_t)WPB * wbuf_floats(CPW, d)) * sizeof(float);
+  if (shm > 163840) return hipErrorInvalidConfiguration;
+  auto kern = arwmh_step_kernel<DMAX, M, EXACT>;
+  // persistent grid: as many blocks as are co-resident (each wave then walks
+  // chain groups wave, wave + total_waves, ...)
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, kBlockStep, shm);
+  if (e != hipSuccess) return e;
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (per_cu < 1) per_cu = 1;
+  const int64_t need = (n_items + WPB - 1) / WPB;
+  int64_t blocks = (int64_t)cus * per_cu;
+  if (blocks > need) blocks = need;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kBlockStep), shm, s, p);
   return hipGetLastError();
 }
 

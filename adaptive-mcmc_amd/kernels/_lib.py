@@ -13,7 +13,7 @@ import subprocess
 import torch  # noqa: F401  (loads the HIP runtime libamh.so binds against)
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "lib", "libamh.so")
+LIB_PATH = os.environ.get("AMH_LIB_PATH") or os.path.join(_PKG, "lib", "libamh.so")
 CSRC = os.path.join(_PKG, "csrc")
 
 AMH_MODEL_GAUSSIAN = 1

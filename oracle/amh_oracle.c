@@ -369,16 +369,16 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
   for (int r = 0; r < G; ++r) sacc[r] = 0.0f;
   if (!revert) {
     /* sweep 2: U'_rj = U_rj + c_j w_r^(j+1); as_change terms */
-    float ed[ORC_DMAX], qe[ORC_DMAX];
-    for (int r = 0; r < d; ++r) { ed[r] = s->dl[r] * el; qe[r] = qq[r] * e1; }
+    /* L'_rj e1 - L_rj e0 = U_rj (q_j e1 - dl_j e0) + (c_j q_j e1) w_r^(j+1) */
+    float ac[ORC_DMAX], bc[ORC_DMAX];
+    for (int r = 0; r < d; ++r) { ac[r] = (qq[r] * e1) - (s->dl[r] * el); bc[r] = (cc[r] * qq[r]) * e1; }
     for (int r = 0; r < d; ++r) w[r] = delta[r];
     for (int j = 0; j < d; ++j) {
       for (int r = 0; r < d; ++r) {
         const float uo = s->U[r][j];
         w[r] = fmaf(-ws[j], uo, w[r]);
         const float un = fmaf(cc[j], w[r], uo);
-        const float told = uo * ed[j];
-        const float tt = fmaf(un, qe[j], -told);
+        const float tt = fmaf(uo, ac[j], bc[j] * w[r]);
         sacc[r] = fmaf(tt, tt, sacc[r]);
         s->U[r][j] = un;
       }
@@ -387,13 +387,12 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
     for (int r = 0; r < d; ++r) s->dl[r] = qq[r];
     s->updated = 1;
   } else {
-    float ed0[ORC_DMAX], ed1[ORC_DMAX];
-    for (int r = 0; r < d; ++r) { ed0[r] = s->dl[r] * el; ed1[r] = s->dl[r] * e1; }
+    /* factor unchanged: L_rj (e1 - e0) = U_rj (dl_j e1 - dl_j e0) */
+    float ac[ORC_DMAX];
+    for (int r = 0; r < d; ++r) ac[r] = (s->dl[r] * e1) - (s->dl[r] * el);
     for (int j = 0; j < d; ++j)
       for (int r = 0; r < d; ++r) {
-        const float uo = s->U[r][j];
-        const float told = uo * ed0[j];
-        const float tt = fmaf(uo, ed1[j], -told);
+        const float tt = s->U[r][j] * ac[j];
         sacc[r] = fmaf(tt, tt, sacc[r]);
       }
     s->asc = sqrtf(group_sum(sacc, G));
