@@ -569,21 +569,36 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     const uint32_t wave_bytes = (uint32_t)CPW * P * 4u;
     const Buf Lout(uniform_ptr(p.out.scale + first * P), wave_bytes);
     const Buf Lin(uniform_ptr(p.in.scale + first * P), wave_bytes);
-    static_for<DMAX>([&](auto J) {
-      constexpr int j = J;
-      if (j < d) {
-        const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
-        const uint32_t vo = off_from<G, j>(vrow, oob, rr);
-        float v;
-        if (any_upd) {
-          v = U[j] * Gp::template bcast<j>(dl);
-        } else {
-          v = Lin.ld(vo, so);
+    // (the branch is outside the column loop: a per-column select between a
+    // load and a product made the compiler wait vmcnt(0) before every store)
+    if (any_upd) {
+      static_for<DMAX>([&](auto J) {
+        constexpr int j = J;
+        if (j < d) {
+          const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
+          Lout.st(U[j] * Gp::template bcast<j>(dl), off_from<G, j>(vrow, oob, rr), so);
         }
-        Lout.st(v, vo, so);
-      }
-      column_fence<j>();
-    });
+        column_fence<j>();
+      });
+    } else {
+      // verbatim copy: all loads first (into the now dead U registers), then
+      // all stores, so the copy waits for memory once
+      static_for<(DMAX + 15) / 16>([&](auto B) {  // batches of 16 columns
+        static_for<16>([&](auto K) {
+          constexpr int j = 16 * B + K;
+          if constexpr (j < DMAX) {
+            if (j < d) U[j] = Lin.ld(off_from<G, j>(vrow, oob, rr), (uint32_t)(col_off(d, j) - j) * 4u);
+          }
+        });
+        static_for<16>([&](auto K) {
+          constexpr int j = 16 * B + K;
+          if constexpr (j < DMAX) {
+            if (j < d) Lout.st(U[j], off_from<G, j>(vrow, oob, rr), (uint32_t)(col_off(d, j) - j) * 4u);
+          }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      });
+    }
     if (chain_ok) {
       if (act) {
         p.out.z[chain * d + r] = z;
