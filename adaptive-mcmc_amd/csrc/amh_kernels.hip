@@ -168,9 +168,52 @@ __device__ __forceinline__ int64_t col_off(int d, int j) {
 
 #define HALF_LOG_2PI 0.918938533204672742f
 
+// ------------------------------------------------------ model-data LDS reads --
+// Model data staged in LDS is never a DMA destination, but the compiler cannot
+// tell it from the step kernel's prefetch buffers (one LDS allocation): a plain
+// LDS load makes it wait vmcnt(0) for the in-flight buffer_load..lds prefetch.
+// These reads are issued as asm (invisible to the wait-count pass) and
+// completed by lds_wait(), which ties the loaded values so no use can be
+// scheduled before the wait.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const float lds_cfloat;
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(lds_cfloat*)p;
+}
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_ld4(uint32_t a) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ float lds_ld1(uint32_t a) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void lds_wait(T& a, T& b, T& c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c));
+}
+template <class T>
+__device__ __forceinline__ void lds_wait(T& a, T& b, T& c, T& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
 // ------------------------------------------------------------------ models --
 // Every model: static potential(x_r, r, d, args, lds) -> U (same value in all
 // lanes of the group), evaluated with all lanes converged.
+
+// Model interface (every potential runs with all lanes of the group
+// converged and returns the same U in every lane of the group):
+//   lds_bytes(args, d)             model data staged in LDS per block
+//   stage(lds, args, d)            block-cooperative staging
+//   Ctx prepare(args, d, r)        per-lane constants, loaded once per kernel
+//   potential(x_r, r, d, ctx, lds) U(x)
+// Nothing is read from global memory inside potential() for the Gaussian,
+// eight-schools and kidiq models: inside the step kernel a global load would
+// make the compiler drain the in-flight LDS-DMA prefetch (vmcnt(0)).
 
 template <int G>
 struct GaussianM {
@@ -178,8 +221,11 @@ struct GaussianM {
   // lds[r * ld + j] with ld = d rounded up to 4 plus 4 floats of padding, so
   // lane r reads its own row with ds_read_b128 (4 columns per read) and the
   // 16-B slots of the 16 lanes of a read group fall on distinct banks.
+  struct Ctx {
+    float mr, c0;
+  };
   static __host__ __device__ int ld(int d) { return ((d + 3) & ~3) + 4; }
-  static __host__ __device__ size_t lds_bytes(int d) { return (size_t)d * ld(d) * sizeof(float); }
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int d) { return (size_t)d * ld(d) * sizeof(float); }
   static __device__ void stage(float* lds, const ModelArgs& m, int d) {
     const float* P = m.data + d;
     const int L = ld(d);
@@ -188,41 +234,56 @@ struct GaussianM {
       lds[k] = (col < d) ? P[row * d + col] : 0.0f;
     }
   }
-  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
-                                                    const float* lds) {
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int d, int r) {
+    return Ctx{(r < d) ? m.data[r] : 0.0f, m.data[d + d * d]};
+  }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float* lds) {
     const bool act = r < d;
-    const float mr = act ? m.data[r] : 0.0f;
-    const float diff = act ? x - mr : 0.0f;
-    const float4* prow = reinterpret_cast<const float4*>(lds + (act ? r : 0) * ld(d));
-    float y = 0.0f;
-    static_for<(G + 3) / 4>([&](auto J4) {
-      constexpr int j4 = J4;
-      if (4 * j4 < d) {
-        const float4 pv = prow[j4];
-        const float pj[4] = {pv.x, pv.y, pv.z, pv.w};
-        static_for<4>([&](auto K) {
-          constexpr int j = 4 * j4 + K;
+    const float diff = act ? x - c.mr : 0.0f;
+    const uint32_t prow = lds_addr(lds + (act ? r : 0) * ld(d));
+    // partial sums over columns j mod 4 (four independent FMA chains); the
+    // row is read 16 columns at a time (four ds_read_b128 then one wait)
+    float y4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    static_for<(G + 15) / 16>([&](auto B) {
+      constexpr int b = B;
+      if (16 * b < d) {
+        f32x4 pv[4];
+        static_for<4>([&](auto Q) {
+          // a block that starts below d lies inside the padded row
+          pv[Q] = (4 * (4 * b + Q) < d) ? lds_ld4<16 * (4 * b + Q)>(prow) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        });
+        lds_wait(pv[0], pv[1], pv[2], pv[3]);
+        static_for<16>([&](auto K) {
+          constexpr int j = 16 * b + K;
           if constexpr (j < G) {
-            if (j < d) y = fmaf(act ? pj[K] : 0.0f, Grp<G>::template bcast<j>(diff), y);
+            if (j < d) y4[K & 3] = fmaf(act ? pv[K / 4][K % 4] : 0.0f, Grp<G>::template bcast<j>(diff), y4[K & 3]);
           }
         });
-        if ((j4 & 3) == 3) __builtin_amdgcn_sched_barrier(0);  // bound LDS reads in flight
+        __builtin_amdgcn_sched_barrier(0);
       }
     });
+    const float y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
     const float q = act ? diff * y : 0.0f;
     const float S = Grp<G>::sum(q);
-    return (0.5f * S) + m.data[d + d * d];
+    return (0.5f * S) + c.c0;
   }
 };
 
 template <int G>
 struct EightSchoolsM {
   // z = [mu, log tau, theta_base (J)]; data = [y (J) | sigma (J) | log sigma (J)]
-  static __host__ __device__ size_t lds_bytes(int) { return 0; }
+  struct Ctx {
+    float y, sg, lsg;  // school r - 2 (lanes 2 .. d-1)
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int) { return 0; }
   static __device__ void stage(float*, const ModelArgs&, int) {}
-  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
-                                                    const float*) {
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int d, int r) {
     const int J = d - 2;
+    const bool sch = r >= 2 && r < d;
+    const int j = sch ? r - 2 : 0;
+    return Ctx{sch ? m.data[j] : 0.0f, sch ? m.data[J + j] : 1.0f, sch ? m.data[2 * J + j] : 0.0f};
+  }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float*) {
     const float mu = Grp<G>::template bcast<0>(x);
     const float lt = Grp<G>::template bcast<1>(x);
     const float tau = amh_expf(lt);
@@ -234,11 +295,10 @@ struct EightSchoolsM {
       const float t = tau / 5.0f;
       v = ((-0.451582705289454865f - 1.60943791243410037f) - amh_log1pf(t * t)) + lt;
     } else if (r < d) {
-      const int j = r - 2;
       const float th = x;
       const float lpt = (-0.5f * (th * th)) - HALF_LOG_2PI;
-      const float e = (m.data[j] - (mu + tau * th)) / m.data[J + j];
-      const float lpy = ((-0.5f * (e * e)) - m.data[2 * J + j]) - HALF_LOG_2PI;
+      const float e = (c.y - (mu + tau * th)) / c.sg;
+      const float lpy = ((-0.5f * (e * e)) - c.lsg) - HALF_LOG_2PI;
       v = lpt + lpy;
     }
     return -Grp<G>::sum(v);
@@ -247,23 +307,31 @@ struct EightSchoolsM {
 
 template <int G>
 struct KidiqM {
-  // z = [beta0, beta1, beta2, log sigma]; data = [kid | hs | iq] (N each)
-  static __host__ __device__ size_t lds_bytes(int) { return 0; }
-  static __device__ void stage(float*, const ModelArgs&, int) {}
-  static __device__ __forceinline__ float potential(float x, int r, int, const ModelArgs& m,
-                                                    const float*) {
-    const int64_t N = m.n;
+  // z = [beta0, beta1, beta2, log sigma]; data = [kid | hs | iq] (N each),
+  // staged in LDS
+  struct Ctx {
+    int64_t N;
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs& m, int) { return (size_t)(3 * m.n) * sizeof(float); }
+  static __device__ void stage(float* lds, const ModelArgs& m, int) {
+    for (int64_t k = threadIdx.x; k < 3 * m.n; k += blockDim.x) lds[k] = m.data[k];
+  }
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int, int) { return Ctx{m.n}; }
+  static __device__ __forceinline__ float potential(float x, int r, int, const Ctx& c, const float* lds) {
+    const int64_t N = c.N;
     const float b0 = Grp<G>::template bcast<0>(x), b1 = Grp<G>::template bcast<1>(x);
     const float b2 = Grp<G>::template bcast<2>(x), ls = Grp<G>::template bcast<3>(x);
     const float sg = amh_expf(ls);
     const float isg = 1.0f / sg;
-    const float* kid = m.data;
-    const float* hs = m.data + N;
-    const float* iq = m.data + 2 * N;
+    const uint32_t a0 = lds_addr(lds);
+    const uint32_t nb = (uint32_t)N * 4u;
     float acc = 0.0f;
     for (int64_t n = r; n < N; n += G) {
-      const float mu = fmaf(b2, iq[n], fmaf(b1, hs[n], b0));
-      const float e = (kid[n] - mu) * isg;
+      const uint32_t an = a0 + (uint32_t)n * 4u;
+      float kid = lds_ld1<0>(an), hs = lds_ld1<0>(an + nb), iq = lds_ld1<0>(an + 2u * nb);
+      lds_wait(kid, hs, iq);
+      const float mu = fmaf(b2, iq, fmaf(b1, hs, b0));
+      const float e = (kid - mu) * isg;
       acc = fmaf(e, e, acc);
     }
     const float S = Grp<G>::sum(acc);
@@ -282,16 +350,20 @@ __device__ __forceinline__ float lp_student3(float x, float loc, float scale, fl
 template <int G>
 struct DiamondsM {
   // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)]
-  // Straight VALU restatement (parity path); the MFMA GEMM path lives in
-  // amh_diamonds.hip.
-  static __host__ __device__ size_t lds_bytes(int) { return 0; }
+  // Straight VALU restatement (parity path; the data stream from L2).
+  struct Ctx {
+    int64_t N;
+    const float* data;
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int) { return 0; }
   static __device__ void stage(float*, const ModelArgs&, int) {}
-  static __device__ __forceinline__ float potential(float x, int r, int d, const ModelArgs& m,
-                                                    const float*) {
-    const int64_t N = m.n;
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int, int) { return Ctx{m.n, m.data}; }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float*) {
+    const int64_t N = c.N;
+    const float* data = c.data;
     const int Kc = d - 2;
-    const float* X = m.data;
-    const float* Y = m.data + N * Kc;
+    const float* X = data;
+    const float* Y = data + N * Kc;
     float xb[G];
     static_for<G>([&](auto J) { xb[J] = Grp<G>::template bcast<J>(x); });
     const float icpt = xb[0];
@@ -345,6 +417,28 @@ __device__ __forceinline__ int64_t item_chain(int64_t item) {
 // gamma_n beyond the host-built table (n >= 2^20): same bits, kept out of line
 // so its double-precision constants do not occupy registers in the step loop.
 __device__ __noinline__ float lr_gamma_slow(int32_t n, float a) { return amh_lr_gamma(n, a); }
+
+// gamma_n from the host-built table through the scalar cache (constant
+// address space): a vector load here would drain the LDS-DMA prefetch.
+typedef __attribute__((address_space(4))) const float const_float;
+
+template <int G>
+__device__ __forceinline__ float lookup_gamma(const StepParams& p, int32_t n) {
+  const const_float* tab = (const const_float*)p.gamma_tab;
+  if constexpr (G == 64) {
+    const int32_t nu = __builtin_amdgcn_readfirstlane(n);
+    return (nu < p.gamma_tab_n) ? tab[nu] : lr_gamma_slow(nu, p.a);
+  } else {
+    float g = 0.0f;
+    const int gi_lane = lane_id() / G;
+    static_for<64 / G>([&](auto GI) {
+      const int32_t ng = __builtin_amdgcn_readlane(n, GI * G);
+      const float gv = (ng < p.gamma_tab_n) ? tab[ng] : lr_gamma_slow(ng, p.a);
+      g = (gi_lane == GI) ? gv : g;
+    });
+    return g;
+  }
+}
 
 // ------------------------------------------------------------ buffer I/O --
 // Raw buffer descriptor over one wave's chain block: the base is wave-uniform
@@ -526,6 +620,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   const int d = EXACT ? DMAX : p.d;
   M<G>::stage(lds, p.model, d);
   __syncthreads();
+  const auto mctx = M<G>::prepare(p.model, d, lane_id() & (G - 1));
 
   const int64_t C = p.C;
   const uint32_t P = (uint32_t)(d * (d + 1) / 2);
@@ -533,7 +628,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   const int64_t wave = (int64_t)blockIdx.x * (kBlockStep / 64) + threadIdx.x / 64;
   const int64_t wstride = (int64_t)gridDim.x * (kBlockStep / 64);
   const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));  // wave-uniform
-  float* wb = lds + ((M<G>::lds_bytes(d) / sizeof(float) + 3) & ~(size_t)3) +
+  float* wb = lds + ((M<G>::lds_bytes(p.model, d) / sizeof(float) + 3) & ~(size_t)3) +
               (size_t)wave_in_block * wbuf_floats(CPW, d);
   const float* wL = wb;
   const float* wz = wb + wbuf_L(CPW, d);
@@ -547,7 +642,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   // issued after the wait, so the next wait never has to drain them.
   float U[DMAX];
   float dl = 0.0f, z = 0.0f, mu = 0.0f, pe = 0.0f, macc = 0.0f, lam = 0.0f, asc = 0.0f;
-  int32_t it = 0, nacc = 0;
+  int32_t it = 0, nacc = 0, acc0 = 0;
   uint32_t k0 = 0, k1 = 0;
   bool updated = false;
   int64_t prev = -1;  // item whose state the registers hold
@@ -612,7 +707,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         p.out.as_change[chain] = asc;
         p.out.rng_key[2 * chain] = k0;
         p.out.rng_key[2 * chain + 1] = k1;
-        if (p.accept_count != nullptr) p.accept_count[chain] += nacc;
+        if (p.accept_count != nullptr) p.accept_count[chain] = acc0 + nacc;  // loaded with the item
       }
     }
   };
@@ -658,6 +753,8 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       z = act ? wz[g * d + r] : 0.0f;
       mu = act ? wm[g * d + r] : 0.0f;
       it = __float_as_int(wsc[0 * CPW + g]);
+      if constexpr (G == 64) it = __builtin_amdgcn_readfirstlane(it);  // wave-uniform: scalar table lookups
+      acc0 = (p.accept_count != nullptr && chain_ok && r == 0) ? p.accept_count[chain] : 0;
       pe = wsc[1 * CPW + g];
       macc = wsc[2 * CPW + g];
       lam = wsc[3 * CPW + g];
@@ -672,23 +769,35 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
+#ifndef AMH_ABLATE_RNG
       const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
       const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
       const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+#else
+      const float xi = act ? (float)((r * 7 + it) % 13) * 0.1f - 0.6f : 0.0f;
+      const float u = (float)(it % 10) * 0.1f;
+#endif
 
       // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
       //      L xi = U (dl * xi)
       const float el = amh_expf(lam);
       const float eta = dl * xi;
-      float acc = 0.0f;
+      // four interleaved partial sums (columns j mod 4): four independent
+      // FMA chains instead of one 64-long dependency chain
+      float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       static_for<DMAX>([&](auto J) {
-        if (J < d) acc = fmaf(U[J], Gp::template bcast<J>(eta), acc);
+        if (J < d) a4[J & 3] = fmaf(U[J], Gp::template bcast<J>(eta), a4[J & 3]);
         column_fence<J, 16>();
       });
+      const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
       const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
 
       // ---- potential, NaN -> +inf (arwmh.py:169-171)
-      float pep = M<G>::potential(zp, r, d, p.model, lds);
+#ifndef AMH_ABLATE_POT
+      float pep = M<G>::potential(zp, r, d, mctx, lds);
+#else
+      float pep = Gp::sum(zp * zp);
+#endif
       if (amh_isnan(pep)) pep = INFINITY;
 
       // ---- accept / reject (arwmh.py:173-178)
@@ -702,7 +811,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       // ---- schedule (arwmh.py:180-185)
       const int32_t itr = it + 1;
       const int32_t n = (it < p.W) ? itr : itr - p.W;
-      const float gamma = (n < p.gamma_tab_n) ? p.gamma_tab[n] : lr_gamma_slow(n, p.a);
+      const float gamma = lookup_gamma<G>(p, n);
       const float maccn = macc + (alpha - macc) / (float)n;
 
       // ---- mean and step size (arwmh.py:188-189, 193)
@@ -721,6 +830,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       // sweep 1: w*_j = w_j when column j is applied (forward solve U w* = delta)
       float w = delta;
       float ws = 0.0f;
+#ifndef AMH_ABLATE_SWEEP1
       static_for<DMAX>([&](auto J) {
         if (J < d) {
           const float wj = Gp::template bcast<J>(w);
@@ -729,6 +839,9 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         }
         column_fence<J>();
       });
+#else
+      ws = w * U[3];
+#endif
 
       // per-column scalars, one column per lane; b_j by exclusive scan
       const float gw2 = act ? gamma * (ws * ws) : 0.0f;
@@ -745,8 +858,13 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       // per-column quantities, and every off-diagonal entry is finite whenever
       // they are ("keep-L rule").  So the keep-L test of
       // arwmh.py:191 is decided before the factor is touched.
+#ifndef AMH_ABLATE_SWEEP2
       const bool revert = Gp::any(act && amh_isnan(dnew));
+#else
+      const bool revert = Gp::any(act && amh_isnan(dnew)) || true;
+#endif
       float sacc = 0.0f;
+      float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // as_change partial sums (columns j mod 4)
       if (!revert) {
         // sweep 2: U'_rj = U_rj + c_j w_r^{(j+1)};  as_change terms
         //   L'_rj e1 - L_rj e0 = U'_rj (q_j e1) - U_rj (dl_j e0)
@@ -764,11 +882,12 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
             w = fmaf(-wj, uo, w);
             const float un = fmaf(cj, w, uo);
             const float tt = fmaf(uo, aj, bj * w);
-            sacc = fmaf(tt, tt, sacc);
+            s4[J & 3] = fmaf(tt, tt, s4[J & 3]);
             U[J] = un;
           }
           column_fence<J>();
         });
+        sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
         asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
         dl = act ? q : 0.0f;
         updated = true;
@@ -778,10 +897,11 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         static_for<DMAX>([&](auto J) {
           if (J < d) {
             const float tt = U[J] * Gp::template bcast<J>(ac);
-            sacc = fmaf(tt, tt, sacc);
+            s4[J & 3] = fmaf(tt, tt, s4[J & 3]);
           }
           column_fence<J>();
         });
+        sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
         asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
       }
 
@@ -821,6 +941,7 @@ __global__ __launch_bounds__(kBlock) void arwmh_init_kernel(InitParams p) {
   const int d = EXACT ? DMAX : p.d;
   M<G>::stage(lds, p.model, d);
   __syncthreads();
+  const auto mctx = M<G>::prepare(p.model, d, lane_id() & (G - 1));
   const int r = Gp::r();
   const bool act = r < d;
   const int64_t C = p.C;
@@ -845,7 +966,7 @@ __global__ __launch_bounds__(kBlock) void arwmh_init_kernel(InitParams p) {
         z0 = (v < -2.0f) ? -2.0f : v;
       }
     }
-    const float pe0 = M<G>::potential(z0, r, d, p.model, lds);
+    const float pe0 = M<G>::potential(z0, r, d, mctx, lds);
     if (chain_ok) {
       float* Lout = p.out.scale + chain * P;
       if (act) {
@@ -876,6 +997,7 @@ __global__ __launch_bounds__(kBlock) void potential_kernel(PotParams p) {
   const int d = EXACT ? DMAX : p.d;
   M<G>::stage(lds, p.model, d);
   __syncthreads();
+  const auto mctx = M<G>::prepare(p.model, d, lane_id() & (G - 1));
   const int r = Gp::r();
   const bool act = r < d;
   const int64_t C = p.n;
@@ -887,7 +1009,7 @@ __global__ __launch_bounds__(kBlock) void potential_kernel(PotParams p) {
     const bool chain_ok = chain < C;
     const int64_t cl = chain_ok ? chain : C - 1;
     const float x = act ? p.z[cl * d + r] : 0.0f;
-    const float pe = M<G>::potential(x, r, d, p.model, lds);
+    const float pe = M<G>::potential(x, r, d, mctx, lds);
     if (chain_ok && r == 0) p.pe[chain] = pe;
   }
 }
@@ -904,6 +1026,7 @@ __global__ __launch_bounds__(kBlock) void sample_pnx_kernel(PnxParams p) {
   const int d = EXACT ? DMAX : p.d;
   M<G>::stage(lds, p.model, d);
   __syncthreads();
+  const auto mctx = M<G>::prepare(p.model, d, lane_id() & (G - 1));
   const int r = Gp::r();
   const bool act = r < d;
   const int64_t C = p.n_points * p.n_samples;
@@ -927,7 +1050,7 @@ __global__ __launch_bounds__(kBlock) void sample_pnx_kernel(PnxParams p) {
     const amh_u32x4 kk = amh_philox4x32_10((uint32_t)cl, (uint32_t)((uint64_t)cl >> 32), 0u, AMH_TAG_SPLIT,
                                            p.key0, p.key1);
     float z = act ? p.x[pt * d + r] : 0.0f;
-    float pe = M<G>::potential(z, r, d, p.model, lds);
+    float pe = M<G>::potential(z, r, d, mctx, lds);
     for (int32_t t = 0; t < p.n; ++t) {
       const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)t, 0u, AMH_TAG_STEP, kk.v[0], kk.v[1]);
       const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
@@ -937,7 +1060,7 @@ __global__ __launch_bounds__(kBlock) void sample_pnx_kernel(PnxParams p) {
         if (J < d) acc = fmaf(A[J], Gp::template bcast<J>(xi), acc);
       });
       const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
-      float pep = M<G>::potential(zp, r, d, p.model, lds);
+      float pep = M<G>::potential(zp, r, d, mctx, lds);
       if (amh_isnan(pep)) pep = INFINITY;
       const float ex = amh_expf(pe - pep);
       const float alpha = (ex > 1.0f) ? 1.0f : ex;
@@ -973,7 +1096,7 @@ hipError_t launch_step(const StepParams& p, hipStream_t s) {
   constexpr int WPB = kBlockStep / 64;
   const int d = EXACT ? DMAX : p.d;
   const int64_t n_items = (p.C + CPW - 1) / CPW;
-  const size_t model_floats = (M<DMAX>::lds_bytes(d) / sizeof(float) + 3) & ~(size_t)3;
+  const size_t model_floats = (M<DMAX>::lds_bytes(p.model, d) / sizeof(float) + 3) & ~(size_t)3;
   const size_t shm = (model_floats + (size_t)WPB * wbuf_floats(CPW, d)) * sizeof(float);
   if (shm > 163840) return hipErrorInvalidConfiguration;
   auto kern = arwmh_step_kernel<DMAX, M, EXACT>;
@@ -997,7 +1120,7 @@ hipError_t launch_step(const StepParams& p, hipStream_t s) {
 template <int DMAX, template <int> class M, bool EXACT>
 hipError_t launch_init(const InitParams& p, hipStream_t s) {
   const int64_t n_items = (p.C + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
-  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  const size_t shm = M<DMAX>::lds_bytes(p.model, EXACT ? DMAX : p.d);
   hipLaunchKernelGGL((arwmh_init_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
                      shm, s, p);
   return hipGetLastError();
@@ -1006,7 +1129,7 @@ hipError_t launch_init(const InitParams& p, hipStream_t s) {
 template <int DMAX, template <int> class M, bool EXACT>
 hipError_t launch_pot(const PotParams& p, hipStream_t s) {
   const int64_t n_items = (p.n + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
-  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  const size_t shm = M<DMAX>::lds_bytes(p.model, EXACT ? DMAX : p.d);
   hipLaunchKernelGGL((potential_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
                      shm, s, p);
   return hipGetLastError();
@@ -1015,7 +1138,7 @@ hipError_t launch_pot(const PotParams& p, hipStream_t s) {
 template <int DMAX, template <int> class M, bool EXACT>
 hipError_t launch_pnx(const PnxParams& p, hipStream_t s) {
   const int64_t n_items = (p.n_points * p.n_samples + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;
-  const size_t shm = M<DMAX>::lds_bytes(EXACT ? DMAX : p.d);
+  const size_t shm = M<DMAX>::lds_bytes(p.model, EXACT ? DMAX : p.d);
   hipLaunchKernelGGL((sample_pnx_kernel<DMAX, M, EXACT>), dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock),
                      shm, s, p);
   return hipGetLastError();

@@ -104,8 +104,9 @@ static float pot_gaussian(const orc_cfg* cfg, const float* x, int G) {
   for (int r = 0; r < G; ++r) diff[r] = (r < d) ? x[r] - m[r] : 0.0f;
   for (int r = 0; r < G; ++r) {
     if (r >= d) { q[r] = 0.0f; continue; }
-    float y = 0.0f;
-    for (int j = 0; j < d; ++j) y = fmaf(P[r * d + j], diff[j], y); /* row r (LDS layout) */
+    float y4[4] = {0.0f, 0.0f, 0.0f, 0.0f}; /* partial sums over j mod 4 (kernel order) */
+    for (int j = 0; j < d; ++j) y4[j & 3] = fmaf(P[r * d + j], diff[j], y4[j & 3]); /* row r */
+    const float y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
     q[r] = diff[r] * y;
   }
   const float S = group_sum(q, G);
@@ -304,8 +305,9 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
   float eta[ORC_DMAX], zp[ORC_DMAX];
   for (int r = 0; r < d; ++r) eta[r] = s->dl[r] * xi[r];
   for (int r = 0; r < d; ++r) {
-    float acc = 0.0f;
-    for (int j = 0; j < d; ++j) acc = fmaf(s->U[r][j], eta[j], acc);
+    float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f}; /* partial sums over j mod 4 (kernel order) */
+    for (int j = 0; j < d; ++j) a4[j & 3] = fmaf(s->U[r][j], eta[j], a4[j & 3]);
+    const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
     zp[r] = s->z[r] + fmaf(el, acc, cfg->eps * xi[r]);
   }
   /* arwmh.py:169-171 */
@@ -365,8 +367,8 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
     dnew[r] = fmaf(cc[r], 0.0f, one[r]) * qq[r];
     revert |= amh_isnan(dnew[r]);
   }
-  float sacc[ORC_DMAX];
-  for (int r = 0; r < G; ++r) sacc[r] = 0.0f;
+  float sacc[ORC_DMAX], s4[ORC_DMAX][4]; /* as_change partial sums over j mod 4 */
+  for (int r = 0; r < G; ++r) { sacc[r] = 0.0f; s4[r][0] = s4[r][1] = s4[r][2] = s4[r][3] = 0.0f; }
   if (!revert) {
     /* sweep 2: U'_rj = U_rj + c_j w_r^(j+1); as_change terms */
     /* L'_rj e1 - L_rj e0 = U_rj (q_j e1 - dl_j e0) + (c_j q_j e1) w_r^(j+1) */
@@ -379,10 +381,11 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
         w[r] = fmaf(-ws[j], uo, w[r]);
         const float un = fmaf(cc[j], w[r], uo);
         const float tt = fmaf(uo, ac[j], bc[j] * w[r]);
-        sacc[r] = fmaf(tt, tt, sacc[r]);
+        s4[r][j & 3] = fmaf(tt, tt, s4[r][j & 3]);
         s->U[r][j] = un;
       }
     }
+    for (int r = 0; r < d; ++r) sacc[r] = (s4[r][0] + s4[r][1]) + (s4[r][2] + s4[r][3]);
     s->asc = sqrtf(group_sum(sacc, G));
     for (int r = 0; r < d; ++r) s->dl[r] = qq[r];
     s->updated = 1;
@@ -393,8 +396,9 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
     for (int j = 0; j < d; ++j)
       for (int r = 0; r < d; ++r) {
         const float tt = s->U[r][j] * ac[j];
-        sacc[r] = fmaf(tt, tt, sacc[r]);
+        s4[r][j & 3] = fmaf(tt, tt, s4[r][j & 3]);
       }
+    for (int r = 0; r < d; ++r) sacc[r] = (s4[r][0] + s4[r][1]) + (s4[r][2] + s4[r][3]);
     s->asc = sqrtf(group_sum(sacc, G));
   }
   s->i = itr;
