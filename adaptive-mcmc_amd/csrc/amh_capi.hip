@@ -105,9 +105,9 @@ int amh_create(const amh_config* cfg, int device, amh_handle** out) {
 }
 
 int amh_destroy(amh_handle* h) {
-  if (h && h->gamma_tab) {
+  if (h) {
     (void)hipSetDevice(h->device);
-    (void)hipFree(h->gamma_tab);
+    if (h->gamma_tab) (void)hipFree(h->gamma_tab);
   }
   delete h;
   return AMH_OK;
@@ -232,4 +232,10 @@ int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint3
   return AMH_OK;
 }
 
+#ifdef AMH_STAMPS
+// diagnostic build only: copy the step kernel's per-wave phase stamps
+int amh_diag_stamps(void* host, int64_t bytes) {
+  return amh::diag_stamps_copy(host, (size_t)bytes) == hipSuccess ? 0 : -1;
+}
+#endif
 }  // extern "C"

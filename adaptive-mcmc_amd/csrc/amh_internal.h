@@ -68,5 +68,8 @@ hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);
 hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, uint32_t* out,
                           hipStream_t s);
+#ifdef AMH_STAMPS
+hipError_t diag_stamps_copy(void* host, size_t bytes);
+#endif
 
 }  // namespace amh

@@ -595,6 +595,41 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
   }
 }
 
+// ------------------------------------------------------- phase stamps --
+// Diagnostic build only (-DAMH_STAMPS, tools/stamps.py): per-wave cycle
+// totals of the step kernel's phases, read back with amh_diag_stamps().
+#ifdef AMH_STAMPS
+constexpr int kStampWaves = 1 << 16;
+constexpr int kStampSlots = 8;  // wait, store, lds->reg, prefetch, compute, tail, items, wall
+__device__ unsigned long long g_stamps[kStampWaves * kStampSlots];
+hipError_t diag_stamps_copy(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#define AMH_STAMP_INIT                             \
+  unsigned long long st_acc[kStampSlots] = {0};    \
+  unsigned long long st_t0 = __builtin_amdgcn_s_memtime(); \
+  unsigned long long st_prev = st_t0;
+#define AMH_STAMP(k)                                          \
+  {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    st_acc[k] += t_ - st_prev;                                \
+    st_prev = t_;                                             \
+  }
+#define AMH_STAMP_COUNT(k) st_acc[k] += 1;
+#define AMH_STAMP_FLUSH(w)                                                                         \
+  {                                                                                                \
+    st_acc[7] = __builtin_amdgcn_s_memtime() - st_t0;                                              \
+    if ((w) < kStampWaves && lane_id() < kStampSlots) g_stamps[(w) * kStampSlots + lane_id()] = 0; \
+    if ((w) < kStampWaves && lane_id() == 0)                                                       \
+      for (int k_ = 0; k_ < kStampSlots; ++k_) g_stamps[(w) * kStampSlots + k_] = st_acc[k_];      \
+  }
+#else
+#define AMH_STAMP_INIT
+#define AMH_STAMP(k)
+#define AMH_STAMP_COUNT(k)
+#define AMH_STAMP_FLUSH(w)
+#endif
+
 // -------------------------------------------------------------- step kernel --
 // One or more ARWMH transitions (arwmh.py:140-207) per chain with the state
 // held in registers between steps.
@@ -611,6 +646,20 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
 // needs no per-column masks: the w_r of a row is zeroed exactly when its own
 // column passes (w - w*1), which keeps the upper triangle at exact zeros.
 // L = U diag(dl) is formed only when the state is written back.
+// Step-kernel LDS, in floats: [ model data | WPB wave buffers | ticket ]
+template <int G, template <int> class M>
+__host__ __device__ __forceinline__ size_t step_wbuf_off(const ModelArgs& m, int d) {
+  return (M<G>::lds_bytes(m, d) / sizeof(float) + 3) & ~(size_t)3;
+}
+template <int G, template <int> class M>
+__host__ __device__ __forceinline__ size_t tickets_off(const ModelArgs& m, int d) {
+  return step_wbuf_off<G, M>(m, d) + (size_t)(kBlockStep / 64) * wbuf_floats(Geo<G>::CPW, d);
+}
+template <int G, template <int> class M>
+__host__ __device__ __forceinline__ size_t step_lds_bytes(const ModelArgs& m, int d) {
+  return (tickets_off<G, M>(m, d) + 4) * sizeof(float);
+}
+
 template <int DMAX, template <int> class M, bool EXACT>
 __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   constexpr int G = DMAX;
@@ -619,17 +668,16 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   extern __shared__ float lds[];
   const int d = EXACT ? DMAX : p.d;
   M<G>::stage(lds, p.model, d);
+  if (threadIdx.x == 0) lds[tickets_off<G, M>(p.model, d)] = 0.0f;  // ticket counter (bits 0)
   __syncthreads();
   const auto mctx = M<G>::prepare(p.model, d, lane_id() & (G - 1));
 
   const int64_t C = p.C;
   const uint32_t P = (uint32_t)(d * (d + 1) / 2);
   const int64_t n_items = (C + CPW - 1) / CPW;
-  const int64_t wave = (int64_t)blockIdx.x * (kBlockStep / 64) + threadIdx.x / 64;
-  const int64_t wstride = (int64_t)gridDim.x * (kBlockStep / 64);
+  [[maybe_unused]] const int64_t wave = (int64_t)blockIdx.x * (kBlockStep / 64) + threadIdx.x / 64;
   const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));  // wave-uniform
-  float* wb = lds + ((M<G>::lds_bytes(p.model, d) / sizeof(float) + 3) & ~(size_t)3) +
-              (size_t)wave_in_block * wbuf_floats(CPW, d);
+  float* wb = lds + step_wbuf_off<G, M>(p.model, d) + (size_t)wave_in_block * wbuf_floats(CPW, d);
   const float* wL = wb;
   const float* wz = wb + wbuf_L(CPW, d);
   const float* wm = wz + wbuf_zd(CPW, d);
@@ -712,10 +760,29 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     }
   };
 
-  int64_t item = wave;
-  if (item < n_items) prefetch_item<G>(p, item * CPW, d, wb, lane_id());
+  // Chain groups are split into one contiguous range per block; inside a
+  // block the waves take groups from an LDS ticket counter, so waves that
+  // lose the SIMD's issue arbitration simply process fewer groups (static
+  // striding left the slowest wave ~1.4x behind the mean).  The ticket for
+  // the group after next is drawn right after a prefetch is issued.  (A
+  // single device-wide counter was tried: its global atomics serialise and
+  // stall the memory pipeline behind them.)
+  const int64_t blk_lo = n_items * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t blk_hi = n_items * ((int64_t)blockIdx.x + 1) / gridDim.x;
+  const uint32_t tk_addr = lds_addr(lds) + (uint32_t)(tickets_off<G, M>(p.model, d) * sizeof(float));
+  auto ticket = [&]() -> int64_t {
+    uint32_t v = 0;
+    if (lane_id() == 0) {
+      asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tk_addr), "v"(1u) : "memory");
+    }
+    return blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+  };
+  AMH_STAMP_INIT
+  int64_t item = ticket();
+  int64_t nxt = item < blk_hi ? ticket() : blk_hi;
 
-  for (; item < n_items; item += wstride) {
+  if (item < blk_hi) prefetch_item<G>(p, item * CPW, d, wb, lane_id());
+  for (; item < blk_hi;) {
     // Every lane-dependent quantity is derived from an opaque copy of the lane
     // id inside the loop: otherwise the compiler hoists dozens of per-column
     // addresses and masks out of this persistent loop and runs out of VGPRs.
@@ -730,7 +797,9 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     const bool chain_ok = chain < C;
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this item's DMA has landed
+    AMH_STAMP(0)
     if (prev >= 0) store_item(prev, lane);
+    AMH_STAMP(1)
 
     // ---- state: LDS -> registers
     {
@@ -763,7 +832,13 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       k1 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g + 1]);
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): buffer consumed before it is refilled
-    if (item + wstride < n_items) prefetch_item<G>(p, (item + wstride) * CPW, d, wb, lane);
+    AMH_STAMP(2)
+    int64_t nxt2 = blk_hi;
+    if (nxt < blk_hi) {
+      prefetch_item<G>(p, nxt * CPW, d, wb, lane);
+      nxt2 = ticket();
+    }
+    AMH_STAMP(3)
 
     nacc = 0;
     updated = false;
@@ -923,12 +998,19 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     }
 
     prev = item;
+    item = nxt;
+    nxt = nxt2;
+    AMH_STAMP(4)
+    AMH_STAMP_COUNT(6)
   }
   if (prev >= 0) {
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
     store_item(prev, lane);
   }
+  __builtin_amdgcn_s_waitcnt(0);
+  AMH_STAMP(5)
+  AMH_STAMP_FLUSH(wave)
 }
 
 // -------------------------------------------------------------- init kernel --
@@ -1096,8 +1178,7 @@ hipError_t launch_step(const StepParams& p, hipStream_t s) {
   constexpr int WPB = kBlockStep / 64;
   const int d = EXACT ? DMAX : p.d;
   const int64_t n_items = (p.C + CPW - 1) / CPW;
-  const size_t model_floats = (M<DMAX>::lds_bytes(p.model, d) / sizeof(float) + 3) & ~(size_t)3;
-  const size_t shm = (model_floats + (size_t)WPB * wbuf_floats(CPW, d)) * sizeof(float);
+  const size_t shm = step_lds_bytes<DMAX, M>(p.model, d);
   if (shm > 163840) return hipErrorInvalidConfiguration;
   auto kern = arwmh_step_kernel<DMAX, M, EXACT>;
   // persistent grid: as many blocks as are co-resident (each wave then walks

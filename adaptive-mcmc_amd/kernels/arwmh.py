@@ -186,10 +186,10 @@ class ARWMH:
     def init(self, rng_key, num_warmup, init_params, model_args, model_kwargs):
         """arwmh.py:84-138: z0 (init_to_uniform unless init_params), pe0 = U(z0),
         loc = z0, scale = I, log_step_size = 0, i = 0."""
-        device_index = _device_index(self._device)
-        device = torch.device("cuda", device_index)
         if self._model is None and init_params is None:
             raise ValueError("Valid value of `init_params` must be provided with `potential_fn`.")
+        device_index = _device_index(self._device)
+        device = torch.device("cuda", device_index)
         self._bind(int(num_warmup), dict(model_kwargs or {}), device_index)
         d = self._dim
         iz = None

@@ -1,0 +1,1 @@
+"""Drivers around the ARWMH kernel (reference python/utils/)."""

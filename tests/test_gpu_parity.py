@@ -119,3 +119,46 @@ def test_headline_size_properties(gpu):
     assert torch.isfinite(dg).all() and (dg > 0).all()
     macc = a.mean_accept_prob.mean().item()
     assert 0.05 < macc < 0.6, macc
+
+
+def test_sharded_equals_unsharded(gpu):
+    """Regime A sharding: two shards run with chain_offset
+    reproduce the unsharded run bit for bit, including a ragged split."""
+    from kernels import ARWMH, PRNGKey
+    from kernels.distributed import shard_range
+    import posteriors as P
+    g = P.correlated_gaussian(64)
+    C = 3001
+    z0 = torch.empty(C, 64, device=gpu).uniform_(-2, 2)
+    full = ARWMH(potential_fn=g, num_chains=C)
+    sf = full.init(PRNGKey(3), 10, z0, (), {})
+    full.sample_(sf, 30)
+    parts = []
+    for r in range(3):
+        off, cnt = shard_range(C, r, 3)
+        k = ARWMH(potential_fn=g, num_chains=cnt, chain_offset=off)
+        s = k.init(PRNGKey(3), 10, z0[off:off + cnt].contiguous(), (), {})
+        k.sample_(s, 30)
+        parts.append(s)
+    torch.cuda.synchronize()
+    assert torch.equal(torch.cat([p.z for p in parts]), sf.z)
+    assert torch.equal(torch.cat([p.adapt_state.scale for p in parts]), sf.adapt_state.scale)
+    assert torch.equal(torch.cat([p.rng_key for p in parts]), sf.rng_key)
+
+
+def test_edge_sizes(gpu, orc):
+    """One chain, a chain count that leaves most of the last work item empty,
+    and d = 1 (the frozen-acceptance model of asumptions_check.ipynb)."""
+    from kernels import ARWMH, PRNGKey
+    import posteriors as P
+    for d, C in ((64, 1), (3, 17), (1, 5), (2, 1)):
+        g = P.correlated_gaussian(d)
+        kw, om = dict(potential_fn=g), orc.Model(orc.GAUSSIAN, d, g.pack("cpu")[0].numpy())
+        k = ARWMH(num_chains=C, **kw)
+        z0 = np.random.default_rng(d).uniform(-2, 2, size=(C, d)).astype(np.float32)
+        st = k.init(PRNGKey(1), 3, torch.as_tensor(z0), (), {})
+        ost = orc.init(om, PRNGKey(1), C, init_z=z0)
+        k.sample_(st, 9)
+        orc.step(om, ost, 9, num_warmup=3)
+        torch.cuda.synchronize()
+        assert_state_bitequal(st, ost, f"d={d} C={C}")
