@@ -58,6 +58,22 @@ def ess_geyer(x: np.ndarray) -> float:
     return float(m * n / max(tau, 1e-12))
 
 
+def measured_traffic(C: int, d: int):
+    """HBM bytes per launch of the step kernel from the newest committed PMC
+    summary for this workload (profiles/<round>_step_kernel.json, written by
+    tools/prof_summary.py from FETCH_SIZE/WRITE_SIZE passes of this bench)."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_step_kernel.json"))):
+        try:
+            j = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if j.get("chains") == C and j.get("dim") == d:
+            best = (j["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
+    return best
+
+
 def cpu_baseline(g, d: int, budget_s: float = 12.0):
     """C oracle (test infrastructure) timed on this host: same step, same
     layout, OpenMP over chains.  Bounded sample: 65,536 chains, as many whole
@@ -177,6 +193,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(g, d)
 
+    traffic = measured_traffic(C, d)
     if rank == 0:
         line = {
             "metric": "chain-steps/sec (whole node) + ESS/sec, 64-dim Gaussian",
@@ -195,7 +212,9 @@ def main():
                                    "per-chain adaptation (BASELINE.json configs[1])",
                        "chains_per_gpu": C, "dim": d, "parallelism": f"chains sharded x{world}, no collective"},
             "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved_gbs / HBM_PEAK_GBS,
+                         "traffic": traffic[0] if traffic else None,
+                         "traffic_source": traffic[1] if traffic else None,
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
             "cpu_baseline": cpu,
             "ess": ess,
