@@ -162,3 +162,36 @@ def test_edge_sizes(gpu, orc):
         orc.step(om, ost, 9, num_warmup=3)
         torch.cuda.synchronize()
         assert_state_bitequal(st, ost, f"d={d} C={C}")
+
+
+@pytest.mark.parametrize("name", ["eight_schools", "gaussian64"])
+def test_gpu_follows_golden(name, gpu):
+    """The device path against the golden vectors of tests/golden (literal
+    float64 restatement): identical accept decisions at every step, states
+    within the tolerances of tests/test_golden.py."""
+    import os
+    import posteriors as P
+    from kernels import ARWMH
+    from test_golden import tol
+    f = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
+    C = f["init_z"].shape[0]
+    if name == "eight_schools":
+        k = ARWMH(model=P.eight_schools, num_chains=C)
+        st = k.init(f["run_key"], 0, torch.as_tensor(f["init_z"]), (), dict(P.EIGHT_SCHOOLS_DATA))
+    else:
+        g = P.correlated_gaussian(64)
+        assert np.array_equal(g.pack("cpu")[0].numpy(), f["model_data"])
+        k = ARWMH(potential_fn=g, num_chains=C)
+        st = k.init(f["run_key"], 0, torch.as_tensor(f["init_z"]), (), {})
+    rec = {int(t): j for j, t in enumerate(f["steps_recorded"])}
+    prev = k.accept_count.clone()
+    for t in range(f["accept"].shape[1]):
+        k.sample_(st, 1)
+        now = k.accept_count.clone()
+        assert np.array_equal((now - prev).bool().cpu().numpy(), f["accept"][:, t]), f"step {t + 1}"
+        prev = now
+        if t + 1 in rec:
+            j, tl = rec[t + 1], tol(t + 1)
+            np.testing.assert_allclose(st.z.cpu().numpy(), f["z"][j], rtol=tl["z"][0], atol=tl["z"][1])
+            np.testing.assert_allclose(st.adapt_state.loc.cpu().numpy(), f["loc"][j], rtol=tl["loc"][0],
+                                       atol=tl["loc"][1])
