@@ -21,6 +21,8 @@ struct amh_handle {
   amh::ModelArgs model{nullptr, 0, 0};
   int64_t n_data = 0;
   float* gamma_tab = nullptr;  // device, kGammaTab entries
+  double* partials = nullptr;  // pooled mode: chunk partial sums (scratch)
+  size_t partials_bytes = 0;
   std::string err;
 };
 
@@ -108,6 +110,7 @@ int amh_destroy(amh_handle* h) {
   if (h) {
     (void)hipSetDevice(h->device);
     if (h->gamma_tab) (void)hipFree(h->gamma_tab);
+    if (h->partials) (void)hipFree(h->partials);
   }
   delete h;
   return AMH_OK;
@@ -229,6 +232,95 @@ int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint3
   if (!key || !out || n < 1 || chain_offset < 0) return fail(nullptr, AMH_EINVAL, "amh_chain_keys: bad arguments");
   hipError_t e = amh::run_chain_keys(key[0], key[1], chain_offset, n, out, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(nullptr, e, "amh_chain_keys");
+  return AMH_OK;
+}
+
+// ------------------------------------------------------- pooled covariance --
+static bool pooled_ok(const amh_pooled_state* s) {
+  return s && s->i && s->z && s->potential_energy && s->rng_key && s->mean_accept_prob && s->loc && s->scale &&
+         s->log_step_size && s->as_change && s->cov;
+}
+
+int amh_pooled_sums_size(int32_t dim, int64_t* v) {
+  if (dim < 1 || dim > 64 || !v) return fail(nullptr, AMH_EINVAL, "amh_pooled_sums_size: bad arguments");
+  *v = (int64_t)dim + (int64_t)dim * (dim + 1) / 2 + 2;
+  return AMH_OK;
+}
+
+int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, float* z_out, float* pe_out,
+                     double* sums, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_stats: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
+  if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1)
+    return fail(h, AMH_EINVAL, "amh_pooled_stats: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
+  const int d = h->cfg.dim;
+  const int cpw = amh::pooled_cpw(num_chains);
+  const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
+  const int64_t n_chunks = (num_chains + chunk - 1) / chunk;
+  const size_t need = (size_t)n_chunks * (size_t)(d + (int64_t)d * (d + 1) / 2 + 2) * sizeof(double);
+  if (need > h->partials_bytes) {
+    if (h->partials) {
+      (void)hipStreamSynchronize((hipStream_t)stream);  // a queued launch may still use the old scratch
+      (void)hipFree(h->partials);
+    }
+    h->partials = nullptr;
+    h->partials_bytes = 0;
+    e = hipMalloc(&h->partials, need);
+    if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipMalloc");
+    h->partials_bytes = need;
+  }
+  amh::PooledStatsParams p{};
+  p.C = num_chains;
+  p.d = d;
+  p.i = in->i;
+  p.z = in->z;
+  p.pe = in->potential_energy;
+  p.keys = in->rng_key;
+  p.mu = in->loc;
+  p.L = in->scale;
+  p.lam = in->log_step_size;
+  p.eps = h->cfg.eps;
+  p.z_out = z_out;
+  p.pe_out = pe_out;
+  p.partials = h->partials;
+  p.model = h->model;
+  e = amh::run_pooled_stats(h->model_id, p, sums, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats");
+  return AMH_OK;
+}
+
+int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
+                      void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_update: null handle");
+  if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipSetDevice");
+  amh::PooledUpdateParams p{};
+  p.d = h->cfg.dim;
+  p.W = h->cfg.num_warmup;
+  p.a = h->cfg.lr_decay;
+  p.target = h->cfg.target_accept_prob;
+  p.sums = sums;
+  p.in = *in;
+  p.out = *out;
+  e = amh::run_pooled_update(p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update");
+  return AMH_OK;
+}
+
+int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, const amh_pooled_state* out,
+                    int32_t n_steps, double* sums, void* stream) {
+  if (n_steps < 0) return fail(h, AMH_EINVAL, "amh_pooled_step: n_steps < 0");
+  const amh_pooled_state* src = in;
+  for (int32_t t = 0; t < n_steps; ++t) {
+    int rc = amh_pooled_stats(h, num_chains, src, out->z, out->potential_energy, sums, stream);
+    if (rc != AMH_OK) return rc;
+    rc = amh_pooled_update(h, sums, src, out, stream);
+    if (rc != AMH_OK) return rc;
+    src = out;
+  }
   return AMH_OK;
 }
 

@@ -1,0 +1,506 @@
+// amh_device.h -- device building blocks shared by the step kernels
+// (amh_kernels.hip: per-chain adaptation; amh_pooled.hip: pooled adaptation):
+// lane-group primitives, model potentials (the PosteriorDB plug-in surface),
+// buffer descriptors and the (model, d) dispatch table.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+#include <utility>
+
+#include "../../include/amh.h"
+#include "../../include/amh_math.h"
+#include "amh_internal.h"
+
+namespace amh {
+
+__device__ __forceinline__ int lane_id() { return (int)__lane_id(); }
+
+// ------------------------------------------------------------ lane groups --
+// Cross-lane primitives inside a group of G lanes (G | 64), built on DPP,
+// ds_swizzle, permlane and readlane so that no lane-address VGPRs are needed.
+// Their association orders are part of the bit spec (oracle: group_sum,
+// group_excl_scan).
+namespace dpp {
+constexpr int quad(int a, int b, int c, int d) { return a | (b << 2) | (c << 4) | (d << 6); }
+constexpr int kRowShr0 = 0x110;
+constexpr int kRowRor0 = 0x120;
+constexpr int kWaveShr1 = 0x138;
+constexpr int kRowBcast15 = 0x142;
+constexpr int kRowBcast31 = 0x143;
+constexpr int kRowNewBcast0 = 0x150;
+}  // namespace dpp
+
+// compile-time unrolled loop: f(std::integral_constant<int, j>) for j < N
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+// Scheduling fence every K unrolled columns: the serial column sweeps have
+// little ILP to gain, and without fences the scheduler hoists independent
+// per-column products (64 of them) and runs out of VGPRs.
+template <int J, int K = 8>
+__device__ __forceinline__ void column_fence() {
+  if constexpr ((J % K) == K - 1) __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int CTRL, int ROWMASK = 0xF, bool BC = true>
+__device__ __forceinline__ float dppf(float old, float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(old), __float_as_int(v), CTRL, ROWMASK, 0xF, BC));
+}
+template <int PATTERN>
+__device__ __forceinline__ float swz(float v) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), PATTERN));
+}
+
+template <int G>
+struct Grp {
+  static_assert(G >= 1 && G <= 64 && (G & (G - 1)) == 0, "group width must be a power of two");
+  static __device__ __forceinline__ int r() { return lane_id() & (G - 1); }
+
+  // value of lane J of this lane's group
+  template <int J>
+  static __device__ __forceinline__ float bcast(float v) {
+    static_assert(J >= 0 && J < G, "lane index out of group");
+    if constexpr (G == 64) {
+      return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), J));
+    } else if constexpr (G == 32) {
+      const int t = __builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::kRowNewBcast0 + (J & 15), 0xF, 0xF, false);
+      const auto sw = __builtin_amdgcn_permlane16_swap(t, t, false, false);
+      return __int_as_float(J < 16 ? sw[0] : sw[1]);
+    } else if constexpr (G == 16) {
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::kRowNewBcast0 + J, 0xF, 0xF, false));
+    } else if constexpr (G == 8) {
+      return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x18 | (J << 5)));
+    } else if constexpr (G == 4) {
+      return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::quad(J, J, J, J), 0xF, 0xF, false));
+    } else if constexpr (G == 2) {
+      return __int_as_float(
+          __builtin_amdgcn_update_dpp(0, __float_as_int(v), dpp::quad(J, J, 2 + J, 2 + J), 0xF, 0xF, false));
+    } else {
+      return v;
+    }
+  }
+  template <int J>
+  static __device__ __forceinline__ uint32_t bcast_u(uint32_t v) {
+    return (uint32_t)__float_as_int(bcast<J>(__int_as_float((int)v)));
+  }
+  // runtime lane index (model code with data-dependent layout)
+  static __device__ __forceinline__ float bcast_rt(float v, int j) {
+    if constexpr (G == 64) {
+      return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
+    } else if constexpr (G == 1) {
+      return v;
+    } else {
+      return __shfl(v, (lane_id() & ~(G - 1)) | j, 64);
+    }
+  }
+
+  // butterfly: for off = 1, 2, 4, ..: x_r = x_r + x_{r ^ off}  (oracle: group_sum)
+  static __device__ __forceinline__ float sum(float v) {
+    if constexpr (G >= 2) v = v + dppf<dpp::quad(1, 0, 3, 2)>(0.0f, v);
+    if constexpr (G >= 4) v = v + dppf<dpp::quad(2, 3, 0, 1)>(0.0f, v);
+    if constexpr (G >= 8) v = v + swz<0x1F | (4 << 10)>(v);
+    if constexpr (G >= 16) v = v + dppf<dpp::kRowRor0 + 8>(0.0f, v);
+    if constexpr (G >= 32) v = v + swz<0x1F | (16 << 10)>(v);
+    if constexpr (G == 64) {
+      // every lane of each 32-lane half holds that half's total here
+      v = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+          __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    }
+    return v;
+  }
+
+  // exclusive scan (oracle: group_excl_scan): shift by one lane, inclusive
+  // Hillis-Steele inside 16-lane rows, then row totals via row_bcast15/31.
+  static __device__ __forceinline__ float excl_scan(float t, int rr) {
+    if constexpr (G == 1) {
+      return 0.0f;
+    } else {
+      float x = dppf<dpp::kWaveShr1>(0.0f, t);
+      if constexpr (G < 64) x = (rr == 0) ? 0.0f : x;
+      if constexpr (G >= 2) { const float y = dppf<dpp::kRowShr0 + 1>(0.0f, x); x = (G >= 16 || rr >= 1) ? x + y : x; }
+      if constexpr (G >= 4) { const float y = dppf<dpp::kRowShr0 + 2>(0.0f, x); x = (G >= 16 || rr >= 2) ? x + y : x; }
+      if constexpr (G >= 8) { const float y = dppf<dpp::kRowShr0 + 4>(0.0f, x); x = (G >= 16 || rr >= 4) ? x + y : x; }
+      if constexpr (G >= 16) { const float y = dppf<dpp::kRowShr0 + 8>(0.0f, x); x = x + y; }
+      if constexpr (G >= 32) { x = x + dppf<dpp::kRowBcast15, 0xA>(0.0f, x); }
+      if constexpr (G == 64) { x = x + dppf<dpp::kRowBcast31, 0xC>(0.0f, x); }
+      return x;
+    }
+  }
+
+  static __device__ __forceinline__ bool any(bool p) {
+    const unsigned long long m = __ballot(p);
+    if constexpr (G == 64) {
+      return m != 0ull;
+    } else {
+      const int g0 = lane_id() & ~(G - 1);
+      constexpr unsigned long long gm = (1ull << G) - 1ull;
+      return ((m >> g0) & gm) != 0ull;
+    }
+  }
+};
+
+// packed column-major lower triangle: column j starts at j*d - j(j-1)/2
+__device__ __forceinline__ int64_t col_off(int d, int j) {
+  return (int64_t)j * d - (int64_t)j * (j - 1) / 2;
+}
+
+#define HALF_LOG_2PI 0.918938533204672742f
+
+// ------------------------------------------------------ model-data LDS reads --
+// Model data staged in LDS is never a DMA destination, but the compiler cannot
+// tell it from the step kernel's prefetch buffers (one LDS allocation): a plain
+// LDS load makes it wait vmcnt(0) for the in-flight buffer_load..lds prefetch.
+// These reads are issued as asm (invisible to the wait-count pass) and
+// completed by lds_wait(), which ties the loaded values so no use can be
+// scheduled before the wait.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const float lds_cfloat;
+__device__ __forceinline__ uint32_t lds_addr(const float* p) {
+  return (uint32_t)(uintptr_t)(lds_cfloat*)p;
+}
+template <int OFF>
+__device__ __forceinline__ f32x4 lds_ld4(uint32_t a) {
+  f32x4 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ float lds_ld1(uint32_t a) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "n"(OFF));
+  return v;
+}
+template <class T>
+__device__ __forceinline__ void lds_wait(T& a, T& b, T& c) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c));
+}
+template <class T>
+__device__ __forceinline__ void lds_wait(T& a, T& b, T& c, T& d) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
+}
+
+// ------------------------------------------------------------------ models --
+// Every model: static potential(x_r, r, d, args, lds) -> U (same value in all
+// lanes of the group), evaluated with all lanes converged.
+
+// Model interface (every potential runs with all lanes of the group
+// converged and returns the same U in every lane of the group):
+//   lds_bytes(args, d)             model data staged in LDS per block
+//   stage(lds, args, d)            block-cooperative staging
+//   Ctx prepare(args, d, r)        per-lane constants, loaded once per kernel
+//   potential(x_r, r, d, ctx, lds) U(x)
+// Nothing is read from global memory inside potential() for the Gaussian,
+// eight-schools and kidiq models: inside the step kernel a global load would
+// make the compiler drain the in-flight LDS-DMA prefetch (vmcnt(0)).
+
+template <int G>
+struct GaussianM {
+  // data = [m (d) | P (d*d) | c0].  P is symmetric; LDS holds row r of P at
+  // lds[r * ld + j] with ld = d rounded up to 4 plus 4 floats of padding, so
+  // lane r reads its own row with ds_read_b128 (4 columns per read) and the
+  // 16-B slots of the 16 lanes of a read group fall on distinct banks.
+  struct Ctx {
+    float mr, c0;
+  };
+  static __host__ __device__ int ld(int d) { return ((d + 3) & ~3) + 4; }
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int d) { return (size_t)d * ld(d) * sizeof(float); }
+  static __device__ void stage(float* lds, const ModelArgs& m, int d) {
+    const float* P = m.data + d;
+    const int L = ld(d);
+    for (int k = threadIdx.x; k < d * L; k += blockDim.x) {
+      const int row = k / L, col = k - row * L;
+      lds[k] = (col < d) ? P[row * d + col] : 0.0f;
+    }
+  }
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int d, int r) {
+    return Ctx{(r < d) ? m.data[r] : 0.0f, m.data[d + d * d]};
+  }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float* lds) {
+    const bool act = r < d;
+    const float diff = act ? x - c.mr : 0.0f;
+    const uint32_t prow = lds_addr(lds + (act ? r : 0) * ld(d));
+    // partial sums over columns j mod 4 (four independent FMA chains); the
+    // row is read 16 columns at a time (four ds_read_b128 then one wait)
+    float y4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    static_for<(G + 15) / 16>([&](auto B) {
+      constexpr int b = B;
+      if (16 * b < d) {
+        f32x4 pv[4];
+        static_for<4>([&](auto Q) {
+          // a block that starts below d lies inside the padded row
+          pv[Q] = (4 * (4 * b + Q) < d) ? lds_ld4<16 * (4 * b + Q)>(prow) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        });
+        lds_wait(pv[0], pv[1], pv[2], pv[3]);
+        static_for<16>([&](auto K) {
+          constexpr int j = 16 * b + K;
+          if constexpr (j < G) {
+            if (j < d) y4[K & 3] = fmaf(act ? pv[K / 4][K % 4] : 0.0f, Grp<G>::template bcast<j>(diff), y4[K & 3]);
+          }
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    });
+    const float y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
+    const float q = act ? diff * y : 0.0f;
+    const float S = Grp<G>::sum(q);
+    return (0.5f * S) + c.c0;
+  }
+};
+
+template <int G>
+struct EightSchoolsM {
+  // z = [mu, log tau, theta_base (J)]; data = [y (J) | sigma (J) | log sigma (J)]
+  struct Ctx {
+    float y, sg, lsg;  // school r - 2 (lanes 2 .. d-1)
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int d, int r) {
+    const int J = d - 2;
+    const bool sch = r >= 2 && r < d;
+    const int j = sch ? r - 2 : 0;
+    return Ctx{sch ? m.data[j] : 0.0f, sch ? m.data[J + j] : 1.0f, sch ? m.data[2 * J + j] : 0.0f};
+  }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float*) {
+    const float mu = Grp<G>::template bcast<0>(x);
+    const float lt = Grp<G>::template bcast<1>(x);
+    const float tau = amh_expf(lt);
+    float v = 0.0f;
+    if (r == 0) {
+      const float t = mu / 5.0f;
+      v = ((-0.5f * (t * t)) - 1.60943791243410037f) - HALF_LOG_2PI;
+    } else if (r == 1) {
+      const float t = tau / 5.0f;
+      v = ((-0.451582705289454865f - 1.60943791243410037f) - amh_log1pf(t * t)) + lt;
+    } else if (r < d) {
+      const float th = x;
+      const float lpt = (-0.5f * (th * th)) - HALF_LOG_2PI;
+      const float e = (c.y - (mu + tau * th)) / c.sg;
+      const float lpy = ((-0.5f * (e * e)) - c.lsg) - HALF_LOG_2PI;
+      v = lpt + lpy;
+    }
+    return -Grp<G>::sum(v);
+  }
+};
+
+template <int G>
+struct KidiqM {
+  // z = [beta0, beta1, beta2, log sigma]; data = [kid | hs | iq] (N each),
+  // staged in LDS
+  struct Ctx {
+    int64_t N;
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs& m, int) { return (size_t)(3 * m.n) * sizeof(float); }
+  static __device__ void stage(float* lds, const ModelArgs& m, int) {
+    for (int64_t k = threadIdx.x; k < 3 * m.n; k += blockDim.x) lds[k] = m.data[k];
+  }
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int, int) { return Ctx{m.n}; }
+  static __device__ __forceinline__ float potential(float x, int r, int, const Ctx& c, const float* lds) {
+    const int64_t N = c.N;
+    const float b0 = Grp<G>::template bcast<0>(x), b1 = Grp<G>::template bcast<1>(x);
+    const float b2 = Grp<G>::template bcast<2>(x), ls = Grp<G>::template bcast<3>(x);
+    const float sg = amh_expf(ls);
+    const float isg = 1.0f / sg;
+    const uint32_t a0 = lds_addr(lds);
+    const uint32_t nb = (uint32_t)N * 4u;
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      const uint32_t an = a0 + (uint32_t)n * 4u;
+      float kid = lds_ld1<0>(an), hs = lds_ld1<0>(an + nb), iq = lds_ld1<0>(an + 2u * nb);
+      lds_wait(kid, hs, iq);
+      const float mu = fmaf(b2, iq, fmaf(b1, hs, b0));
+      const float e = (kid - mu) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    const float S = Grp<G>::sum(acc);
+    const float t = sg / 2.5f;
+    const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpr = ((-0.451582705289454865f - 0.916290731874155065f) - amh_log1pf(t * t)) + ls;
+    return -(ll + lpr);
+  }
+};
+
+__device__ __forceinline__ float lp_student3(float x, float loc, float scale, float c) {
+  const float t = (x - loc) / scale;
+  return c - 2.0f * amh_log1pf((t * t) / 3.0f);
+}
+
+template <int G>
+struct DiamondsM {
+  // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)]
+  // Straight VALU restatement (parity path; the data stream from L2).
+  struct Ctx {
+    int64_t N;
+    const float* data;
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int, int) { return Ctx{m.n, m.data}; }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float*) {
+    const int64_t N = c.N;
+    const float* data = c.data;
+    const int Kc = d - 2;
+    const float* X = data;
+    const float* Y = data + N * Kc;
+    float xb[G];
+    static_for<G>([&](auto J) { xb[J] = Grp<G>::template bcast<J>(x); });
+    const float icpt = xb[0];
+    const float ls = Grp<G>::bcast_rt(x, Kc + 1);
+    const float sg = amh_expf(ls);
+    const float isg = 1.0f / sg;
+    float acc = 0.0f;
+    for (int64_t n = r; n < N; n += G) {
+      float mu = 0.0f;
+#pragma unroll
+      for (int k = 0; k < G - 1; ++k) {
+        if (k >= Kc) continue;
+        mu = fmaf(X[n * Kc + k], xb[1 + k], mu);
+      }
+      const float e = (Y[n] - (icpt + mu)) * isg;
+      acc = fmaf(e, e, acc);
+    }
+    const float S = Grp<G>::sum(acc);
+    const float bb = (r >= 1 && r <= Kc) ? x * x : 0.0f;
+    const float B = Grp<G>::sum(bb);
+    const float cst = -3.30347394261755545f;
+    const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+    const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+    const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+    return -(((ll + lpb) + lpi) + lps);
+  }
+};
+
+// --------------------------------------------------------------- geometry --
+constexpr int kBlock = 256;       // 4 waves (init / potential / sample_Pnx kernels)
+constexpr int kBlockStep = 1024;  // 16 waves per CU share one staged copy of the model data
+#ifndef AMH_STEP_MIN_WAVES
+#define AMH_STEP_MIN_WAVES 1  // waves per SIMD the step kernel must fit (VGPR budget)
+#endif
+
+template <int G>
+struct Geo {
+  static constexpr int CPW = 64 / G;  // chains per wave
+};
+
+// Chain owned by this lane's group for work item `item`; clamped to C-1 so
+// that tail groups run converged on valid memory and simply do not store.
+template <int G>
+__device__ __forceinline__ int64_t item_chain(int64_t item) {
+  int64_t c = item * Geo<G>::CPW + (lane_id() / G);
+  if constexpr (G == 64) c = (int64_t)__builtin_amdgcn_readfirstlane((int)c);  // wave-uniform
+  return c;
+}
+
+// gamma_n beyond the host-built table (n >= 2^20): same bits, kept out of line
+// so its double-precision constants do not occupy registers in the step loop.
+static __device__ __noinline__ float lr_gamma_slow(int32_t n, float a) { return amh_lr_gamma(n, a); }
+
+// gamma_n from the host-built table through the scalar cache (constant
+// address space): a vector load here would drain the LDS-DMA prefetch.
+typedef __attribute__((address_space(4))) const float const_float;
+
+template <int G>
+__device__ __forceinline__ float lookup_gamma(const StepParams& p, int32_t n) {
+  const const_float* tab = (const const_float*)p.gamma_tab;
+  if constexpr (G == 64) {
+    const int32_t nu = __builtin_amdgcn_readfirstlane(n);
+    return (nu < p.gamma_tab_n) ? tab[nu] : lr_gamma_slow(nu, p.a);
+  } else {
+    float g = 0.0f;
+    const int gi_lane = lane_id() / G;
+    static_for<64 / G>([&](auto GI) {
+      const int32_t ng = __builtin_amdgcn_readlane(n, GI * G);
+      const float gv = (ng < p.gamma_tab_n) ? tab[ng] : lr_gamma_slow(ng, p.a);
+      g = (gi_lane == GI) ? gv : g;
+    });
+    return g;
+  }
+}
+
+// ------------------------------------------------------------ buffer I/O --
+// Raw buffer descriptor over one wave's chain block: the base is wave-uniform
+// (SGPRs), per-lane offsets are 32-bit VGPRs and the per-column part of an
+// offset is an SGPR, so the 64 column loads of a chain share one VGPR.  Lanes
+// that must not touch memory get an out-of-range voffset (loads return 0,
+// stores are dropped by the hardware range check).
+constexpr uint32_t kOOB = 0x80000000u;
+
+struct Buf {
+  __amdgpu_buffer_rsrc_t rs;
+  __device__ __forceinline__ Buf(const void* base, uint32_t bytes) {
+    rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+  }
+  __device__ __forceinline__ float ld(uint32_t voff, uint32_t soff) const {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, 0));
+  }
+  __device__ __forceinline__ void st(float v, uint32_t voff, uint32_t soff) const {
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, 0);
+  }
+};
+
+__device__ __forceinline__ const void* uniform_ptr(const void* p) {
+  const uint64_t u = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)u);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(u >> 32));
+  return (const void*)(((uint64_t)hi << 32) | lo);
+}
+
+// v_writelane through the LLVM intrinsic (no clang builtin in ROCm 7.2)
+__device__ int amh_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+
+// lane J of the group takes `v` (uniform in the group), other lanes keep `old`
+template <int G, int J>
+__device__ __forceinline__ float capture(float old, float v, int rr) {
+  if constexpr (G == 64) {
+    return __int_as_float(amh_writelane_i32(__float_as_int(v), J, __float_as_int(old)));
+  } else {
+    return (rr == J) ? v : old;
+  }
+}
+
+
+// Dispatch table over (model, d).  Instantiated shapes:
+//   Gaussian: exact d = 64 (headline), dynamic d <= 1,2,4,8,16,32,64
+//   eight schools: d <= 16;  kidiq: d = 4;  diamonds: d <= 32
+template <template <int> class M, class F>
+static hipError_t dispatch_dim(int d, bool allow_exact64, F&& f) {
+  if (d < 1 || d > 64) return hipErrorInvalidValue;
+  if (d == 64 && allow_exact64) return f.template operator()<64, M, true>();
+  if (d <= 1) return f.template operator()<1, M, false>();
+  if (d <= 2) return f.template operator()<2, M, false>();
+  if (d <= 4) return f.template operator()<4, M, false>();
+  if (d <= 8) return f.template operator()<8, M, false>();
+  if (d <= 16) return f.template operator()<16, M, false>();
+  if (d <= 32) return f.template operator()<32, M, false>();
+  return f.template operator()<64, M, false>();
+}
+
+template <class F>
+static hipError_t dispatch(int model_id, int d, F&& f) {
+  switch (model_id) {
+    case AMH_MODEL_GAUSSIAN:
+      return dispatch_dim<GaussianM>(d, true, f);
+    case AMH_MODEL_EIGHT_SCHOOLS:
+      if (d > 16) return hipErrorInvalidValue;
+      return f.template operator()<16, EightSchoolsM, false>();
+    case AMH_MODEL_KIDIQ:
+      if (d != 4) return hipErrorInvalidValue;
+      return f.template operator()<4, KidiqM, true>();
+    case AMH_MODEL_DIAMONDS:
+      if (d > 32) return hipErrorInvalidValue;
+      return f.template operator()<32, DiamondsM, false>();
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+
+}  // namespace amh

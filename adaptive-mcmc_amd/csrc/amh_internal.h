@@ -62,6 +62,38 @@ struct PnxParams {
   ModelArgs model;
 };
 
+// pooled covariance (amh_pooled.hip)
+constexpr int kPoolWaves = 16;  // waves (of one chain each) per chunk block
+
+// chains each wave of a chunk takes (bit spec: fixes the summation order)
+__host__ __device__ inline int pooled_cpw(int64_t C) {
+  const int64_t c = (C + 4095) / 4096;
+  return c < 1 ? 1 : (c > 16 ? 16 : (int)c);
+}
+
+struct PooledStatsParams {
+  int64_t C;
+  int32_t d;
+  const int32_t* i;
+  const float *z, *pe;
+  const uint32_t* keys;
+  const float *mu, *L, *lam;
+  float eps;
+  float *z_out, *pe_out;
+  double* partials;  // [n_chunks][V]
+  ModelArgs model;
+};
+
+struct PooledUpdateParams {
+  int32_t d, W;
+  float a, target;
+  const double* sums;
+  amh_pooled_state in, out;
+};
+
+hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);
+hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s);
+
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
 hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);

@@ -3,7 +3,8 @@
 
 ASSS / NUTS / SA are outside the accelerated path."""
 from .arwmh import ARWMH, ARWMHAdaptState, ARWMHState, init_to_uniform, pack_scale, packed_size, unpack_scale
+from .pooled import PooledAdaptState, PooledARWMH, PooledState
 from .random import PRNGKey, split
 
 __all__ = ["ARWMH", "ARWMHState", "ARWMHAdaptState", "init_to_uniform", "pack_scale", "unpack_scale",
-           "packed_size", "PRNGKey", "split"]
+           "packed_size", "PRNGKey", "split", "PooledARWMH", "PooledState", "PooledAdaptState"]

@@ -23,7 +23,8 @@ AMH_MODEL_DIAMONDS = 4
 
 # every symbol include/amh.h declares
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",
-           "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys")
+           "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
+           "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step")
 
 
 class AmhConfig(ctypes.Structure):
@@ -75,7 +76,7 @@ def lib():
     L.amh_potential.argtypes = [P, P, P, I64, P]
     L.amh_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, F, I32, P, P]
     L.amh_chain_keys.argtypes = [ctypes.POINTER(ctypes.c_uint32), I64, I64, P, P]
-    for name in EXPORTS:
+    for name in EXPORTS[:10]:
         getattr(L, name).restype = ctypes.c_int if name != "amh_last_error" else ctypes.c_char_p
     _lib = L
     return L

@@ -16,7 +16,9 @@
  *   amh_potential                 potential_fn          arwmh.py:121,170
  *   amh_sample_pnx                ARWMH.sample_Pnx      arwmh.py:230-270
  *   amh_pooled_*                  build-defined pooled-covariance mode
- *                                 (SURVEY.md §8(e)); no reference analogue
+ *                                 (SURVEY.md §8(e)); ARWMH.sample's
+ *                                 adaptation (arwmh.py:180-197) driven by
+ *                                 the statistics of all chains
  *
  * Conventions
  *   - Every pointer in amh_state / model data / outputs is a DEVICE pointer
@@ -127,6 +129,50 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
  * callers can reproduce chain streams. */
 int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint32_t* out,
                    void* stream);
+
+/* ---------------------------------------------------- pooled covariance ----
+ * Regime B (build-defined, no reference analogue): every chain
+ * proposes with ONE shared adapt state, and the adaptation of arwmh.py:180-197
+ * consumes the statistics of all chains (of all ranks):
+ *   mu'  = mu + gamma S_d / N,   Sig' = (1 - gamma) Sig + gamma S_dd / N,
+ *   L'   = chol(Sig') (kept, with Sig, if Sig' is not positive definite),
+ *   lam' = lam + gamma (S_a / N - target), macc' = macc + (S_a / N - macc) / n
+ * where S_d = sum delta_c, S_dd = sum delta_c delta_c^T, S_a = sum alpha_c,
+ * delta_c = z_c' - mu.  With N = 1 this is the reference recurrence.
+ * A step is amh_pooled_stats (per-chain transition + local sums), an
+ * all-reduce(sum) of the sums across ranks by the caller (RCCL through
+ * torch.distributed), then amh_pooled_update on every rank. */
+typedef struct amh_pooled_state {
+  int32_t* i;                 /* [1]      shared iteration                   */
+  float* z;                   /* [C][d]   per chain                          */
+  float* potential_energy;    /* [C]                                         */
+  uint32_t* rng_key;          /* [C][2]   per-chain Philox key               */
+  float* mean_accept_prob;    /* [1]                                         */
+  float* loc;                 /* [d]      shared mu                          */
+  float* scale;               /* [P]      shared L, packed lower             */
+  float* log_step_size;       /* [1]                                         */
+  float* as_change;           /* [1]                                         */
+  double* cov;                /* [P]      shared Sigma (= L L^T), packed     */
+} amh_pooled_state;
+
+/* Number of doubles in the sums vector: d + d(d+1)/2 + 2, laid out as
+ * [S_d (d) | S_dd packed lower (P) | S_a | N]. */
+int amh_pooled_sums_size(int32_t dim, int64_t* v);
+
+/* Per-chain transition with the shared state `in`, z / pe written to
+ * z_out / pe_out (may alias in), and this rank's sums (device, V doubles). */
+int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, float* z_out,
+                     float* pe_out, double* sums, void* stream);
+
+/* Shared-state update from the (all-reduced) sums; writes i, mean accept,
+ * loc, scale, log_step_size, as_change, cov of `out` (may alias `in`). */
+int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state* in,
+                      const amh_pooled_state* out, void* stream);
+
+/* Single-process convenience: n_steps of stats + update (no all-reduce).
+ * sums: device scratch of amh_pooled_sums_size doubles. */
+int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in,
+                    const amh_pooled_state* out, int32_t n_steps, double* sums, void* stream);
 
 #ifdef __cplusplus
 }

@@ -556,3 +556,179 @@ int orc_num_threads(void) {
   return 1;
 #endif
 }
+
+/* ================================================= pooled covariance ==== */
+/* Regime B (build-defined): every chain proposes with ONE
+ * shared adapt state (mu, L, lambda); the adaptation consumes the pooled
+ * statistics of all chains (all ranks):
+ *   S_d = sum_c delta_c,  S_dd = sum_c delta_c delta_c^T,  S_a = sum_c alpha_c
+ *   mu'  = mu + gamma S_d / N
+ *   Sig' = (1 - gamma) Sig + gamma S_dd / N,   L' = chol(Sig')  (else keep)
+ *   lam' = lam + gamma (S_a / N - target),     macc' = macc + (S_a/N - macc)/n
+ * With N = 1 this is the reference recurrence (arwmh.py:180-197) with the
+ * rank-one update replaced by a refactorisation.
+ *
+ * Kernel mirror: one chain per 64-lane wave (G = 64 for every d <= 64);
+ * chunks of 16 waves x cpw consecutive chains; per wave float32 accumulators
+ * over its chains in order, the 16 wave partials of a chunk summed in
+ * double in wave order, chunk partials summed in double in chunk order.
+ * sums layout (V = d + P + 2 doubles): [S_d (d) | S_dd packed col-major (P) |
+ * S_a | N]. */
+#define ORC_POOLED_WAVES 16
+
+int orc_pooled_cpw(int64_t C) {
+  const int64_t c = (C + 4095) / 4096;
+  return c < 1 ? 1 : (c > 16 ? 16 : (int)c);
+}
+
+static float orc_potential_g(const orc_cfg* cfg, const float* x, int G) {
+  switch (cfg->model_id) {
+    case ORC_GAUSSIAN: return pot_gaussian(cfg, x, G);
+    case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
+    case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
+    case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
+    default: return NAN;
+  }
+}
+
+/* Per-chain transition with the shared state; writes z/pe out and the
+ * pooled sums.  i: shared iteration (noise stream position). */
+void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
+                      const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
+                      float* z_out, float* pe_out, double* sums) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const int64_t V = d + P + 2;
+  const int cpw = orc_pooled_cpw(C);
+  const int64_t chunk = (int64_t)ORC_POOLED_WAVES * cpw;
+  const int64_t n_chunks = (C + chunk - 1) / chunk;
+  float L[ORC_DMAX][ORC_DMAX];
+  memset(L, 0, sizeof(L));
+  for (int j = 0; j < d; ++j)
+    for (int r = j; r < d; ++r) L[r][j] = Lpacked[col_off(d, j) + (r - j)];
+  const float el = amh_expf(lam);
+  double* part = (double*)calloc((size_t)(n_chunks * V), sizeof(double));
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t ch = 0; ch < n_chunks; ++ch) {
+    double* acc = part + ch * V;
+    double cnt = 0.0;
+    for (int w = 0; w < ORC_POOLED_WAVES; ++w) {
+      float S[ORC_DMAX][ORC_DMAX], sd[ORC_DMAX], sa = 0.0f;
+      memset(S, 0, sizeof(S));
+      memset(sd, 0, sizeof(sd));
+      for (int t = 0; t < cpw; ++t) {
+        const int64_t c = ch * chunk + (int64_t)w * cpw + t;
+        if (c >= C) continue;
+        cnt += 1.0;
+        const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
+        float xi[ORC_DMAX], zp[ORC_DMAX], zn[ORC_DMAX], delta[ORC_DMAX];
+        uint32_t ubits = 0;
+        for (int r = 0; r < d; ++r) {
+          const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)i, 0u, AMH_TAG_STEP, k0, k1);
+          xi[r] = amh_normal_from_bits(o.v[0]);
+          if (r == 0) ubits = o.v[1];
+        }
+        const float u = amh_unif01_from_bits(ubits);
+        for (int r = 0; r < d; ++r) {
+          float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+          for (int j = 0; j < d; ++j) a4[j & 3] = fmaf(L[r][j], xi[j], a4[j & 3]);
+          const float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+          zp[r] = z[c * d + r] + fmaf(el, a, cfg->eps * xi[r]);
+        }
+        float pep = orc_potential_g(cfg, zp, 64);
+        if (amh_isnan(pep)) pep = INFINITY;
+        const float ex = amh_expf(pe[c] - pep);
+        const float alpha = (ex > 1.0f) ? 1.0f : ex;
+        const int accept = u < alpha;
+        for (int r = 0; r < d; ++r) {
+          zn[r] = accept ? zp[r] : z[c * d + r];
+          delta[r] = zn[r] - mu[r];
+        }
+        for (int r = 0; r < d; ++r) {
+          z_out[c * d + r] = zn[r];
+          sd[r] = sd[r] + delta[r];
+          for (int k = 0; k <= r; ++k) S[r][k] = fmaf(delta[r], delta[k], S[r][k]);
+        }
+        pe_out[c] = accept ? pep : pe[c];
+        sa = sa + alpha;
+      }
+      for (int r = 0; r < d; ++r) acc[r] += (double)sd[r];
+      for (int k = 0; k < d; ++k)
+        for (int r = k; r < d; ++r) acc[d + col_off(d, k) + (r - k)] += (double)S[r][k];
+      acc[d + P] += (double)sa;
+    }
+    acc[d + P + 1] = cnt;
+  }
+  for (int64_t v = 0; v < V; ++v) {
+    double s = 0.0;
+    for (int64_t ch = 0; ch < n_chunks; ++ch) s += part[ch * V + v];
+    sums[v] = s;
+  }
+  free(part);
+}
+
+/* Shared-state update from the (all-reduced) sums.  Returns 1 if the factor
+ * was refactorised, 0 if kept. */
+int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
+                      float* Lpacked, float* lam, float* asc, double* cov) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const double N = sums[d + P + 1];
+  const int32_t it = *i_;
+  const int32_t itr = it + 1;
+  const int32_t n = (it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  const float abar = (float)(sums[d + P] / N);
+  const float maccn = *macc + (abar - *macc) / (float)n;
+  const float lamn = *lam + gamma * (abar - cfg->target_accept_prob);
+  for (int r = 0; r < d; ++r) mu[r] = mu[r] + gamma * (float)(sums[r] / N);
+  const double g = (double)gamma;
+  /* Sig' and its Cholesky factor, lower triangle A[r][k], k <= r */
+  double A[ORC_DMAX][ORC_DMAX];
+  memset(A, 0, sizeof(A));
+  for (int k = 0; k < d; ++k)
+    for (int r = k; r < d; ++r) {
+      const int64_t o = col_off(d, k) + (r - k);
+      const double a = (1.0 - g) * cov[o];
+      const double b = g * (sums[d + o] / N);
+      A[r][k] = a + b;
+    }
+  double Sn[ORC_DMAX][ORC_DMAX];
+  memcpy(Sn, A, sizeof(A));
+  int ok = 1;
+  for (int j = 0; j < d; ++j) {
+    const double piv = A[j][j];
+    if (!(piv > 0.0) || !isfinite(piv)) { ok = 0; break; }
+    const double ljj = sqrt(piv);
+    for (int r = j + 1; r < d; ++r) A[r][j] = A[r][j] / ljj;
+    A[j][j] = ljj;
+    for (int k = j + 1; k < d; ++k)
+      for (int r = k; r < d; ++r) A[r][k] = fma(-A[r][j], A[k][j], A[r][k]);
+  }
+  const float e0 = amh_expf(*lam), e1 = amh_expf(lamn);
+  float part[ORC_DMAX];
+  for (int r = 0; r < 64; ++r) part[r] = 0.0f;
+  for (int r = 0; r < d; ++r) {
+    float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int j = 0; j <= r; ++j) {
+      const float lo = Lpacked[col_off(d, j) + (r - j)];
+      const float ln = ok ? (float)A[r][j] : lo;
+      const float tt = (ln * e1) - (lo * e0);
+      s4[j & 3] = fmaf(tt, tt, s4[j & 3]);
+    }
+    part[r] = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+  }
+  *asc = sqrtf(group_sum(part, 64));
+  if (ok) {
+    for (int k = 0; k < d; ++k)
+      for (int r = k; r < d; ++r) {
+        const int64_t o = col_off(d, k) + (r - k);
+        Lpacked[o] = (float)A[r][k];
+        cov[o] = Sn[r][k];
+      }
+  }
+  *i_ = itr;
+  *macc = maccn;
+  *lam = lamn;
+  return ok;
+}

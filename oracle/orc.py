@@ -71,6 +71,11 @@ def lib():
         L.orc_normal_bits.argtypes = [_P, _P, _I64]
         L.orc_lr_gamma.argtypes = [_P, _F, _P, _I64]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_pooled_cpw.argtypes = [_I64]
+        L.orc_pooled_cpw.restype = ctypes.c_int
+        L.orc_pooled_stats.argtypes = [_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _P, _P, _P]
+        L.orc_pooled_update.argtypes = [_P, _P] + [_P] * 7
+        L.orc_pooled_update.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -213,3 +218,51 @@ def sample_pnx(model: Model, key, x: np.ndarray, loc, scale_packed, log_step_siz
     lib().orc_sample_pnx(ctypes.byref(cfg), _ptr(key), _ptr(x), npts, n_samples, _ptr(loc), _ptr(sp),
                          log_step_size, n, _ptr(out))
     return out
+
+
+# ------------------------------------------------------------- pooled mode --
+def pooled_cpw(C: int) -> int:
+    return lib().orc_pooled_cpw(C)
+
+
+def pooled_stats(model: Model, i: int, z, pe, keys, mu, Lpacked, lam: float, eps: float = 1e-6):
+    """-> (z_out, pe_out, sums[V]) for one pooled step (orc_pooled_stats)."""
+    d = model.d
+    z = _c(z, np.float32).reshape(-1, d)
+    C = z.shape[0]
+    pe = _c(pe, np.float32)
+    keys = _c(keys, np.uint32)
+    mu = _c(mu, np.float32)
+    Lp = _c(Lpacked, np.float32)
+    zo = np.empty_like(z)
+    po = np.empty_like(pe)
+    sums = np.empty(d + d * (d + 1) // 2 + 2, np.float64)
+    cfg = model.cfg(0, 2 / 3, 0.234, eps)
+    lib().orc_pooled_stats(ctypes.byref(cfg), C, int(i), _ptr(z), _ptr(pe), _ptr(keys), _ptr(mu), _ptr(Lp),
+                           ctypes.c_float(lam), _ptr(zo), _ptr(po), _ptr(sums))
+    return zo, po, sums
+
+
+def pooled_update(model: Model, sums, shared: dict, num_warmup: int = 0, lr_decay: float = 2 / 3,
+                  target_accept_prob: float = 0.234) -> int:
+    """In-place update of shared = {i, macc, mu, L, lam, asc, cov} (numpy
+    arrays: i int32[1], macc/lam/asc float32[1], mu float32[d], L float32[P],
+    cov float64[P]).  Returns 1 if refactorised."""
+    cfg = model.cfg(num_warmup, lr_decay, target_accept_prob, 1e-6)
+    sums = _c(sums, np.float64)
+    return lib().orc_pooled_update(ctypes.byref(cfg), _ptr(sums), _ptr(shared["i"]), _ptr(shared["macc"]),
+                                   _ptr(shared["mu"]), _ptr(shared["L"]), _ptr(shared["lam"]), _ptr(shared["asc"]),
+                                   _ptr(shared["cov"]))
+
+
+def pooled_init_shared(d: int) -> dict:
+    P = d * (d + 1) // 2
+    L = np.zeros(P, np.float32)
+    cov = np.zeros(P, np.float64)
+    k = 0
+    for j in range(d):
+        L[k] = 1.0
+        cov[k] = 1.0
+        k += d - j
+    return dict(i=np.zeros(1, np.int32), macc=np.zeros(1, np.float32), mu=np.zeros(d, np.float32), L=L,
+                lam=np.zeros(1, np.float32), asc=np.zeros(1, np.float32), cov=cov)

@@ -1,0 +1,66 @@
+"""Pooled-covariance mode on the GPU (amh_pooled_*) against the oracle
+(orc_pooled_*): per-chain state, the sums vector and the shared state bit
+for bit over several steps (the summation order is part of the spec)."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(kind, d, C, steps, gpu, orc, seed=0):
+    from kernels import PooledARWMH, PRNGKey
+    kw, mk, om = make_case(kind, d)
+    k = PooledARWMH(num_chains=C, **kw)
+    z0 = np.random.default_rng(seed).uniform(-2, 2, size=(C, om.d)).astype(np.float32)
+    st = k.init(PRNGKey(seed), 0, torch.as_tensor(z0), (), mk)
+    ost = orc.init(om, PRNGKey(seed), C, init_z=z0)
+    z, pe, keys = ost.z, ost.potential_energy, ost.rng_key
+    assert np.array_equal(st.rng_key.cpu().numpy().view(np.uint32), keys)
+    assert np.array_equal(st.potential_energy.cpu().numpy().view(np.uint32), pe.view(np.uint32))
+    sh = orc.pooled_init_shared(om.d)
+    for t in range(steps):
+        st = k.sample(st)
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(k._sums.cpu().numpy().view(np.uint64), sums.view(np.uint64),
+                                      err_msg=f"{kind} sums step {t + 1}")
+        orc.pooled_update(om, sums, sh)
+        got = dict(z=st.z, pe=st.potential_energy, mu=st.adapt_state.loc, L=st.adapt_state.scale,
+                   lam=st.adapt_state.log_step_size, macc=st.mean_accept_prob, asc=st.as_change, cov=st.cov,
+                   i=st.i)
+        want = dict(z=z, pe=pe, mu=sh["mu"], L=sh["L"], lam=sh["lam"], macc=sh["macc"], asc=sh["asc"],
+                    cov=sh["cov"], i=sh["i"])
+        for f in got:
+            a = got[f].cpu().numpy()
+            b = np.asarray(want[f])
+            assert a.shape == b.shape, (f, a.shape, b.shape)
+            assert a.tobytes() == b.astype(a.dtype).tobytes(), f"{kind} {f} differs at step {t + 1}"
+    return k, st
+
+
+@pytest.mark.parametrize("kind,d,C,steps", [("gaussian", 64, 3000, 6), ("gaussian", 64, 70000, 3),
+                                            ("gaussian", 7, 517, 8), ("eight_schools", None, 64, 8),
+                                            ("kidiq", None, 100, 5), ("diamonds", None, 40, 3)])
+def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
+    _run(kind, d, C, steps, gpu, orc)
+
+
+def test_pooled_inplace_multistep(gpu, orc):
+    """sample_ (amh_pooled_step, fused host loop) equals repeated sample()."""
+    from kernels import PooledARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", 16)
+    C = 999
+    z0 = torch.empty(C, 16, device=gpu).uniform_(-2, 2)
+    a = PooledARWMH(num_chains=C, **kw)
+    sa = a.init(PRNGKey(4), 5, z0, (), mk)
+    b = PooledARWMH(num_chains=C, **kw)
+    sb = b.init(PRNGKey(4), 5, z0, (), mk)
+    a.sample_(sa, 12)
+    for _ in range(12):
+        sb = b.sample(sb)
+    torch.cuda.synchronize()
+    assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
+    assert torch.equal(sa.cov, sb.cov) and int(sa.i[0]) == 12
