@@ -6,11 +6,11 @@
 //                         shared factor staged in LDS) + the chunk's sums
 //                         S_d, S_dd, S_a (float32 per wave over its chains,
 //                         double across the chunk's waves)
-//   pooled_reduce_kernel  chunk partials -> this rank's sums (double, chunk
-//                         order); ranks then all-reduce them (RCCL)
+//   pooled_reduce_kernel  chunk partials -> this rank's sums (double, fixed
+//                         two-level order); ranks then all-reduce them (RCCL)
 //   pooled_update_kernel  mu, Sigma, lambda, mean-accept update and the
 //                         Cholesky refactorisation of Sigma' (one wave, rows
-//                         in registers, double precision)
+//                         in registers, columns broadcast through LDS, double)
 //
 // The order of every sum is fixed (oracle: orc_pooled_stats/_update), so the
 // result does not depend on which CU runs which chunk.
@@ -50,17 +50,13 @@ template <template <int> class M>
 __host__ __device__ inline size_t pooled_lds_model_floats(const ModelArgs& m, int d) {
   return (M<64>::lds_bytes(m, d) / sizeof(float) + 3) & ~(size_t)3;
 }
+// combine-tree slot: rows r = 0..63 as [S_r0 .. S_rr, sd_r], then sa
+constexpr int kTreeSlot = 64 * 65 / 2 + 64 + 1;
+
 template <template <int> class M>
 __host__ __device__ inline size_t pooled_lds_bytes(const ModelArgs& m, int d) {
   const size_t f = pooled_lds_model_floats<M>(m, d) + (size_t)d * pooled_ld(d);
-  const size_t f8 = (f + 1) & ~(size_t)1;  // 8-B align the double area
-  return f8 * sizeof(float) + (64 * 64 + 64 + 2) * sizeof(double);
-}
-
-__device__ __forceinline__ int64_t packed_col(int d, int64_t o) {  // column of packed index o
-  int k = 0;
-  while (k + 1 < d && col_off(d, k + 1) <= o) ++k;
-  return k;
+  return (f + (size_t)(kPoolWaves / 2) * kTreeSlot) * sizeof(float);
 }
 
 }  // namespace
@@ -75,16 +71,13 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const int64_t V = d + P + 2;
   float* lrow = lds + pooled_lds_model_floats<M>(p.model, d);
-  double* cmb = (double*)(lds + (((size_t)(lrow - lds) + (size_t)d * ld + 1) & ~(size_t)1));
-  double* cmb_sd = cmb + 64 * 64;
-  double* cmb_sa = cmb_sd + 64;
+  float* tree = lrow + (size_t)d * ld;
 
   M<G>::stage(lds, p.model, d);
   for (int k = threadIdx.x; k < d * ld; k += blockDim.x) {
     const int row = k / ld, col = k - row * ld;
     lrow[k] = (col <= row && col < d) ? p.L[col_off(d, col) + (row - col)] : 0.0f;
   }
-  for (int k = threadIdx.x; k < 64 * 64 + 64 + 2; k += blockDim.x) cmb[k] = 0.0;
   __syncthreads();
 
   const int lane = lane_id();
@@ -103,12 +96,26 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
   float S[64];
   static_for<64>([&](auto K) { S[K] = 0.0f; });
   float sd = 0.0f, sa = 0.0f;
-  for (int t = 0; t < cpw; ++t) {
-    const int64_t c = base + t;
-    if (c >= p.C) break;
-    const float z = act ? p.z[c * d + r] : 0.0f;
-    const float pe = p.pe[c];
-    const uint32_t k0 = p.keys[2 * c], k1 = p.keys[2 * c + 1];
+  // this wave's chains [base, end); the next chain's z / pe / key are loaded
+  // while the current one is computed
+  // (buffer descriptors with a wave-uniform base: no 64-bit per-lane
+  // addresses to keep live, lanes r >= d read 0 / store nothing)
+  const int64_t end = (base + cpw < p.C) ? base + cpw : p.C;
+  const uint32_t vr = 4u * (uint32_t)r;
+  auto load_chain = [&](int64_t c, float& zz, float& pp, uint32_t& q0, uint32_t& q1) {
+    const Buf bz(uniform_ptr(p.z + c * d), 4u * (uint32_t)d);
+    zz = bz.ld(vr, 0);
+    pp = p.pe[c];
+    q0 = p.keys[2 * c];
+    q1 = p.keys[2 * c + 1];
+  };
+  float zq = 0.0f, peq = 0.0f;
+  uint32_t k0q = 0, k1q = 0;
+  if (base < end) load_chain(base, zq, peq, k0q, k1q);
+  for (int64_t c = base; c < end; ++c) {
+    const float z = zq, pe = peq;
+    const uint32_t k0 = k0q, k1 = k1q;
+    if (c + 1 < end) load_chain(c + 1, zq, peq, k0q, k1q);
     // noise at the shared stream position (arwmh.py:162-165, 174)
     const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
     const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
@@ -122,7 +129,8 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
     const float alpha = (ex > 1.0f) ? 1.0f : ex;
     const bool accept = u < alpha;
     const float zn = accept ? zp : z;
-    if (act) p.z_out[c * d + r] = zn;
+    const Buf bo(uniform_ptr(p.z_out + c * d), 4u * (uint32_t)d);
+    bo.st(zn, vr, 0);
     if (r == 0) p.pe_out[c] = accept ? pep : pe;
     // pooled statistics (float32 over this wave's chains, in chain order)
     const float delta = act ? zn - mu : 0.0f;
@@ -134,48 +142,85 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
     });
     sa = sa + alpha;
   }
-  // the chunk's waves add their partials in wave order (double)
-  for (int ww = 0; ww < kPoolWaves; ++ww) {
-    if (w == ww) {
+  // The chunk's 16 wave partials are combined by a fixed pairwise tree in
+  // float32 (h = 8, 4, 2, 1: wave w < h adds wave w + h), through LDS slots
+  // holding each row r as [S_r0 .. S_rr, sd_r] (row offset r(r+3)/2) and sa
+  // last; the chunk total is then written in double (oracle mirror).
+  const uint32_t rowoff = (uint32_t)(r * (r + 3) / 2);
+  static_for<4>([&](auto H) {
+    constexpr int h = 8 >> H;
+    if (w >= h && w < 2 * h) {
+      float* slot = tree + (size_t)(w - h) * kTreeSlot;
       if (act) {
         static_for<64>([&](auto K) {
           constexpr int k = K;
-          if (k <= r && k < d) cmb[r * 64 + k] += (double)S[k];
+          if (k <= r) slot[rowoff + k] = S[k];
         });
-        cmb_sd[r] += (double)sd;
+        slot[rowoff + r + 1] = sd;
       }
-      if (lane == 0) *cmb_sa += (double)sa;
+      if (lane == 0) slot[kTreeSlot - 1] = sa;
     }
     __syncthreads();
-  }
-  double* out = p.partials + (int64_t)blockIdx.x * V;
-  const int64_t left = p.C - chunk0;
-  const double cnt = (double)(left < (int64_t)kPoolWaves * cpw ? left : (int64_t)kPoolWaves * cpw);
-  for (int64_t v = threadIdx.x; v < V; v += blockDim.x) {
-    double val;
-    if (v < d) {
-      val = cmb_sd[v];
-    } else if (v < d + P) {
-      const int64_t o = v - d;
-      const int64_t k = packed_col(d, o);
-      const int64_t rr = k + (o - col_off(d, (int)k));
-      val = cmb[rr * 64 + k];
-    } else if (v == d + P) {
-      val = *cmb_sa;
-    } else {
-      val = cnt;
+    if (w < h) {
+      const float* slot = tree + (size_t)w * kTreeSlot;
+      if (act) {
+        static_for<64>([&](auto K) {
+          constexpr int k = K;
+          if (k <= r) S[k] = S[k] + slot[rowoff + k];
+        });
+        sd = sd + slot[rowoff + r + 1];
+      }
+      sa = sa + slot[kTreeSlot - 1];
     }
-    out[v] = val;
+    __syncthreads();
+  });
+  if (w == 0) {
+    double* out = p.partials + (int64_t)blockIdx.x * V;
+    if (act) {
+      static_for<64>([&](auto K) {
+        constexpr int k = K;
+        if (k <= r) out[d + col_off(d, k) + (r - k)] = (double)S[k];
+      });
+      out[r] = (double)sd;
+    }
+    if (lane == 0) {
+      const int64_t left = p.C - chunk0;
+      out[d + P] = (double)sa;
+      out[d + P + 1] = (double)(left < (int64_t)kPoolWaves * cpw ? left : (int64_t)kPoolWaves * cpw);
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void pooled_reduce_kernel(const double* partials, int64_t n_chunks, int64_t V,
-                                                            double* sums) {
-  const int64_t v = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (v >= V) return;
-  double s = 0.0;
-  for (int64_t ch = 0; ch < n_chunks; ++ch) s += partials[ch * V + v];
-  sums[v] = s;
+// Chunk partials -> sums, in a fixed two-level order (oracle mirror):
+// groups of kRedGroup consecutive chunks are summed in chunk order, then the
+// group sums in group order.  Block (v-slice, 16 x 64 threads): thread
+// (grp-lane q, v) sums groups q, q + 16, ... ; one thread per v then adds
+// the group sums in group order.
+constexpr int kRedGroup = 16;
+
+__global__ __launch_bounds__(1024) void pooled_reduce_kernel(const double* partials, int64_t n_chunks, int64_t V,
+                                                             double* sums) {
+  __shared__ double gs[16][64];
+  const int tv = threadIdx.x & 63;
+  const int q = threadIdx.x >> 6;
+  const int64_t v = (int64_t)blockIdx.x * 64 + tv;
+  const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
+  double tot = 0.0;
+  for (int64_t g0 = 0; g0 < n_groups; g0 += 16) {
+    const int64_t g = g0 + q;
+    double s = 0.0;
+    if (v < V && g < n_groups) {
+      const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
+      for (int64_t ch = g * kRedGroup; ch < c1; ++ch) s += partials[ch * V + v];
+    }
+    gs[q][tv] = s;
+    __syncthreads();
+    if (q == 0 && v < V) {
+      for (int k = 0; k < 16 && g0 + k < n_groups; ++k) tot += gs[k][tv];
+    }
+    __syncthreads();
+  }
+  if (q == 0 && v < V) sums[v] = tot;
 }
 
 namespace {
@@ -208,39 +253,44 @@ __global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p)
   const float mun = act ? p.in.loc[r] + gamma * (float)(sums[r] / N) : 0.0f;
   const double g = (double)gamma;
 
-  double A[64];
+  // Sigma' (double) in LDS, row r written by lane r; the old factor's row in
+  // registers.  Every lane loads a valid element (index 0 off the triangle)
+  // so the loads are not serialised behind divergent branches.
+  __shared__ double As[64][65];
   float Lo[64];
   static_for<64>([&](auto K) {
     constexpr int k = K;
-    A[k] = 0.0;
-    Lo[k] = 0.0f;
-    if (k < d && act && k <= r) {
-      const int64_t o = col_off(d, k) + (r - k);
-      const double a = (1.0 - g) * p.in.cov[o];
-      const double b = g * (sums[d + o] / N);
-      A[k] = a + b;
-      Lo[k] = p.in.scale[o];
-    }
+    const bool in = k < d && act && k <= r;
+    const int64_t o = in ? col_off(d, k) + (r - k) : 0;
+    const double cv = p.in.cov[o];
+    const double sv = sums[d + o];
+    const float lv = p.in.scale[o];
+    const double a = (1.0 - g) * cv;
+    const double b = g * (sv / N);
+    As[r][k] = in ? a + b : 0.0;
+    Lo[k] = in ? lv : 0.0f;
   });
+  // Right-looking Cholesky in LDS, lane r = row r: element (r, k) is updated
+  // in column order with fma(-L_rj, L_kj, A_rk) (oracle mirror).
   bool ok = true;
-  static_for<64>([&](auto J) {
-    constexpr int j = J;
-    if (j < d) {
-      const double piv = readlane_f64(A[j], j);
-      ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
-      const double ljj = sqrt(piv);
-      A[j] = (r > j) ? A[j] / ljj : ((r == j) ? ljj : A[j]);
-      static_for<64>([&](auto K) {
-        constexpr int k = K;
-        if constexpr (k > j) {
-          if (k < d) {
-            const double lkj = readlane_f64(A[j], k);
-            A[k] = (r >= k) ? fma(-A[j], lkj, A[k]) : A[k];
-          }
-        }
-      });
+  for (int j = 0; j < d; ++j) {
+    const double piv = As[j][j];
+    ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
+    const double ljj = sqrt(piv);
+    double lrj = 0.0;
+    if (r > j && act) {
+      lrj = As[r][j] / ljj;
+      As[r][j] = lrj;
     }
-  });
+    if (r == j) As[j][j] = ljj;
+#pragma unroll 4
+    for (int k = j + 1; k < d; ++k) {
+      const double lkj = As[k][j];
+      if (r >= k && act) As[r][k] = fma(-lrj, lkj, As[r][k]);
+    }
+  }
+  double A[64];
+  static_for<64>([&](auto K) { A[K] = As[r][K]; });
   const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
   float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   static_for<64>([&](auto J) {
@@ -265,7 +315,7 @@ __global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p)
           const double b = g * (sums[d + o] / N);
           p.out.cov[o] = a + b;
           p.out.scale[o] = (float)A[k];
-        } else {
+        } else {  // kept (rare: gamma = 1 at n = 1, or Sigma' not positive definite)
           p.out.cov[o] = p.in.cov[o];
           p.out.scale[o] = Lo[k];
         }
@@ -294,7 +344,7 @@ hipError_t launch_pooled_stats(const PooledStatsParams& p, double* sums, hipStre
   hipLaunchKernelGGL((pooled_stats_kernel<M, EXACT>), dim3((unsigned)n_chunks), dim3(kPoolWaves * 64), shm, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 255) / 256)), dim3(256), 0, s, p.partials,
+  hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, p.partials,
                      n_chunks, V, sums);
   return hipGetLastError();
 }

@@ -74,6 +74,38 @@ def measured_traffic(C: int, d: int):
     return best
 
 
+def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int):
+    """Regime B (pooled covariance, BASELINE.json configs[4] at N = 8): every
+    step = per-chain transition + local sums, all-reduce(sum) of the sums over
+    RCCL (world > 1), shared refactorisation on every rank."""
+    import torch
+    import torch.distributed as dist
+    from kernels import PooledARWMH, PRNGKey
+    k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=rank * C)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(99 + rank)
+    z0 = (torch.rand(C, g.dim, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = k.init(PRNGKey(0), 0, z0, (), {})
+    k.sample_(st, warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    k.sample_(st, steps)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        wall = float(t.item())
+    return {"value": world * C * steps / wall, "unit": "chain-steps/s", "ms_per_step": wall / steps * 1e3,
+            "steps": steps, "chains_per_gpu": C, "allreduce_doubles": g.dim + g.dim * (g.dim + 1) // 2 + 2,
+            "mean_accept_prob": float(st.mean_accept_prob[0]),
+            "collective": "all_reduce(sum) per step" if world > 1 else "none (1 rank)"}
+
+
 def cpu_baseline(g, d: int, budget_s: float = 12.0):
     """C oracle (test infrastructure) timed on this host: same step, same
     layout, OpenMP over chains.  Bounded sample: 65,536 chains, as many whole
@@ -107,6 +139,7 @@ def main():
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
+    ap.add_argument("--no-pooled", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -189,6 +222,10 @@ def main():
         ess = {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T,
                "seconds": el, "coords": [0, 1, d // 2, d - 1, "U"]}
 
+    pooled = None
+    if not args.no_pooled:
+        pooled = bench_pooled(g, C, dev, rank, world, steps=max(args.steps, 20), warmup=5)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(g, d)
@@ -219,6 +256,7 @@ def main():
             "cpu_baseline": cpu,
             "ess": ess,
             "fused_chain_steps_per_s": fused_rate * world,
+            "pooled": pooled,
         }
         print(json.dumps(line))
     if world > 1:

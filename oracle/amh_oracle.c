@@ -570,8 +570,10 @@ int orc_num_threads(void) {
  *
  * Kernel mirror: one chain per 64-lane wave (G = 64 for every d <= 64);
  * chunks of 16 waves x cpw consecutive chains; per wave float32 accumulators
- * over its chains in order, the 16 wave partials of a chunk summed in
- * double in wave order, chunk partials summed in double in chunk order.
+ * over its chains in order, the 16 wave partials of a chunk combined by a
+ * float32 pairwise tree (w += w + h for h = 8, 4, 2, 1) and converted to
+ * double, chunk partials summed in double in groups of 16
+ * chunks (chunk order), the group sums in group order.
  * sums layout (V = d + P + 2 doubles): [S_d (d) | S_dd packed col-major (P) |
  * S_a | N]. */
 #define ORC_POOLED_WAVES 16
@@ -612,10 +614,12 @@ void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, 
   for (int64_t ch = 0; ch < n_chunks; ++ch) {
     double* acc = part + ch * V;
     double cnt = 0.0;
+    /* per-wave float32 partials: S[w][r][k] (k <= r), sd[w][r], sa[w] */
+    float (*S)[ORC_DMAX][ORC_DMAX] = calloc(ORC_POOLED_WAVES, sizeof(*S));
+    float sd[ORC_POOLED_WAVES][ORC_DMAX], sa[ORC_POOLED_WAVES];
+    memset(sd, 0, sizeof(sd));
+    memset(sa, 0, sizeof(sa));
     for (int w = 0; w < ORC_POOLED_WAVES; ++w) {
-      float S[ORC_DMAX][ORC_DMAX], sd[ORC_DMAX], sa = 0.0f;
-      memset(S, 0, sizeof(S));
-      memset(sd, 0, sizeof(sd));
       for (int t = 0; t < cpw; ++t) {
         const int64_t c = ch * chunk + (int64_t)w * cpw + t;
         if (c >= C) continue;
@@ -646,23 +650,40 @@ void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, 
         }
         for (int r = 0; r < d; ++r) {
           z_out[c * d + r] = zn[r];
-          sd[r] = sd[r] + delta[r];
-          for (int k = 0; k <= r; ++k) S[r][k] = fmaf(delta[r], delta[k], S[r][k]);
+          sd[w][r] = sd[w][r] + delta[r];
+          for (int k = 0; k <= r; ++k) S[w][r][k] = fmaf(delta[r], delta[k], S[w][r][k]);
         }
         pe_out[c] = accept ? pep : pe[c];
-        sa = sa + alpha;
+        sa[w] = sa[w] + alpha;
       }
-      for (int r = 0; r < d; ++r) acc[r] += (double)sd[r];
-      for (int k = 0; k < d; ++k)
-        for (int r = k; r < d; ++r) acc[d + col_off(d, k) + (r - k)] += (double)S[r][k];
-      acc[d + P] += (double)sa;
     }
+    /* pairwise tree over the 16 waves (h = 8, 4, 2, 1), float32 */
+    for (int h = ORC_POOLED_WAVES / 2; h >= 1; h /= 2)
+      for (int w = 0; w < h; ++w) {
+        for (int r = 0; r < d; ++r) {
+          for (int k = 0; k <= r; ++k) S[w][r][k] = S[w][r][k] + S[w + h][r][k];
+          sd[w][r] = sd[w][r] + sd[w + h][r];
+        }
+        sa[w] = sa[w] + sa[w + h];
+      }
+    for (int r = 0; r < d; ++r) acc[r] = (double)sd[0][r];
+    for (int k = 0; k < d; ++k)
+      for (int r = k; r < d; ++r) acc[d + col_off(d, k) + (r - k)] = (double)S[0][r][k];
+    acc[d + P] = (double)sa[0];
+    free(S);
     acc[d + P + 1] = cnt;
   }
+  /* chunk partials: groups of 16 chunks in chunk order, then the groups in
+   * group order (pooled_reduce_kernel) */
+  const int64_t n_groups = (n_chunks + 15) / 16;
   for (int64_t v = 0; v < V; ++v) {
-    double s = 0.0;
-    for (int64_t ch = 0; ch < n_chunks; ++ch) s += part[ch * V + v];
-    sums[v] = s;
+    double tot = 0.0;
+    for (int64_t g = 0; g < n_groups; ++g) {
+      double s = 0.0;
+      for (int64_t ch = g * 16; ch < n_chunks && ch < (g + 1) * 16; ++ch) s += part[ch * V + v];
+      tot += s;
+    }
+    sums[v] = tot;
   }
   free(part);
 }

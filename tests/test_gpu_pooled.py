@@ -64,3 +64,51 @@ def test_pooled_inplace_multistep(gpu, orc):
     torch.cuda.synchronize()
     assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
     assert torch.equal(sa.cov, sb.cov) and int(sa.i[0]) == 12
+
+
+def _gpu_worker(rank, world, port, C, steps, out_path):
+    import os
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks share the box's one GPU
+    import posteriors as P
+    from kernels import PooledARWMH, PRNGKey
+    from kernels.distributed import gather_chains, shard_range
+    g = P.correlated_gaussian(32)
+    off, cnt = shard_range(C, rank, world)
+    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, 32)).astype(np.float32))
+    k = PooledARWMH(potential_fn=g, num_chains=cnt, chain_offset=off, device=torch.device("cuda", 0))
+    st = k.init(PRNGKey(2), 0, z0[off:off + cnt].cuda(), (), {})
+    k.sample_(st, steps)
+    z = gather_chains(st.z.cpu(), C)
+    if rank == 0:
+        np.savez(out_path, z=z.numpy(), L=st.adapt_state.scale.cpu().numpy(), i=st.i.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_pooled_two_ranks(gpu, tmp_path):
+    """The distributed path of PooledARWMH (all-reduce of the sums every
+    step) over 2 ranks equals the 1-rank run up to the association order of
+    the sums."""
+    import socket
+    import torch.multiprocessing as mp
+    import posteriors as P
+    from kernels import PooledARWMH, PRNGKey
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    C, steps = 2001, 25
+    out = str(tmp_path / "g.npz")
+    mp.start_processes(_gpu_worker, args=(2, port, C, steps, out), nprocs=2, join=True, start_method="spawn")
+    r = np.load(out)
+    g = P.correlated_gaussian(32)
+    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, 32)).astype(np.float32))
+    k = PooledARWMH(potential_fn=g, num_chains=C)
+    st = k.init(PRNGKey(2), 0, z0.to(gpu), (), {})
+    k.sample_(st, steps)
+    assert int(r["i"][0]) == steps
+    np.testing.assert_allclose(r["L"], st.adapt_state.scale.cpu().numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(r["z"], st.z.cpu().numpy(), rtol=1e-4, atol=1e-4)
