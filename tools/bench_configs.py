@@ -1,0 +1,98 @@
+"""Per-config throughput of the BASELINE.json single-GPU configurations that
+are not the headline (bench.py measures configs[1]).
+
+  python tools/bench_configs.py [--only diamonds,gauss256,...] [--steps K]
+
+One JSON line per config: chain-steps/s of ARWMH.sample (one launch = one
+transition of every chain, state round trip through HBM), plus the fused
+multi-step rate.  Synthetic data of the reference shapes.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for _p in (os.path.join(ROOT, "adaptive-mcmc_amd"), ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+
+def timed(fn, steps, stream):
+    import torch
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+
+def run_regime_a(name, kernel, C, d, kwargs, steps, warmup, dev):
+    import torch
+    from kernels import PRNGKey
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = kernel.init(PRNGKey(0), 0, z0, (), kwargs)
+    for _ in range(warmup):
+        kernel.sample_(st, 1)
+    wall, kms = timed(lambda: kernel.sample_(st, 1), steps, torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    f0 = time.perf_counter()
+    kernel.sample_(st, 10)
+    torch.cuda.synchronize()
+    fused = C * 10 / (time.perf_counter() - f0)
+    return {"config": name, "chains": C, "dim": d, "steps": steps, "value": C * steps / wall,
+            "unit": "chain-steps/s", "kernel_ms": kms, "fused_chain_steps_per_s": fused,
+            "mean_accept_prob": float(st.mean_accept_prob.mean())}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    args = ap.parse_args()
+    import torch
+    import posteriors as P
+    from kernels import ARWMH, PooledARWMH, PRNGKey
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    want = set(args.only.split(","))
+    if "diamonds" in want:
+        data = P.synthetic_diamonds()
+        C = 262144
+        k = ARWMH(model=P.diamonds, num_chains=C, device=dev)
+        print(json.dumps(run_regime_a("diamonds (BASELINE configs[2])", k, C, P.diamonds.dim(data), data,
+                                      args.steps, args.warmup, dev)), flush=True)
+    if "gauss256" in want:
+        g = P.correlated_gaussian(256, log10_kappa=4.0)
+        C = 32768
+        k = ARWMH(potential_fn=g, num_chains=C, device=dev)
+        print(json.dumps(run_regime_a("gauss256 regime A (BASELINE configs[3])", k, C, 256, {},
+                                      args.steps, args.warmup, dev)), flush=True)
+    for key, d, C, kappa in (("gauss256_pooled", 256, 32768, 4.0), ("pooled64", 64, 65536, 2.0)):
+        if key not in want:
+            continue
+        g = P.correlated_gaussian(d, log10_kappa=kappa)
+        k = PooledARWMH(potential_fn=g, num_chains=C, device=dev)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(9)
+        z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
+        st = k.init(PRNGKey(0), 0, z0, (), {})
+        k.sample_(st, args.warmup)
+        wall, kms = timed(lambda: k.sample_(st, 1), args.steps, torch.cuda.current_stream(dev))
+        print(json.dumps({"config": f"{key} regime B", "chains": C, "dim": d, "steps": args.steps,
+                          "value": C * args.steps / wall, "unit": "chain-steps/s", "ms_per_step": kms,
+                          "mean_accept_prob": float(st.mean_accept_prob[0])}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,7 @@
 #!/bin/bash
-# the whole GPU test suite (one pytest process), then a short bench line
+# the whole GPU test suite (one pytest process)
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -30 gpurun_out/pytest_gpu.log
+timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -40 gpurun_out/pytest_gpu.log
 exit $rc
