@@ -23,6 +23,8 @@ struct amh_handle {
   float* gamma_tab = nullptr;  // device, kGammaTab entries
   double* partials = nullptr;  // pooled mode: chunk partial sums (scratch)
   size_t partials_bytes = 0;
+  float* split_buf = nullptr;  // split path: proposals [C][d] then U(z') [C] (scratch)
+  size_t split_bytes = 0;
   std::string err;
 };
 
@@ -72,6 +74,22 @@ int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d
   }
 }
 
+// device scratch of at least `need` bytes (grown, never shrunk); a queued
+// launch may still read the old buffer, so the stream drains before the free
+int grow(amh_handle* h, float** buf, size_t* have, size_t need, void* stream, const char* where) {
+  if (need <= *have) return AMH_OK;
+  if (*buf) {
+    (void)hipStreamSynchronize((hipStream_t)stream);
+    (void)hipFree(*buf);
+  }
+  *buf = nullptr;
+  *have = 0;
+  hipError_t e = hipMalloc(buf, need);
+  if (e != hipSuccess) return hip_fail(h, e, where);
+  *have = need;
+  return AMH_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -111,6 +129,7 @@ int amh_destroy(amh_handle* h) {
     (void)hipSetDevice(h->device);
     if (h->gamma_tab) (void)hipFree(h->gamma_tab);
     if (h->partials) (void)hipFree(h->partials);
+    if (h->split_buf) (void)hipFree(h->split_buf);
   }
   delete h;
   return AMH_OK;
@@ -151,7 +170,16 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
   p.key1 = key[1];
   p.init_z = init_z;
   p.model = h->model;
-  e = amh::run_init(h->model_id, p, (hipStream_t)stream);
+  if (amh::split_model(h->model_id, p.d)) {
+    // pe0 = U(z0) from the lane-per-chain potential (bit-identical to the group one)
+    e = amh::run_init_nopot(p, (hipStream_t)stream);
+    if (e == hipSuccess) {
+      amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model};
+      e = amh::run_potential_lane(h->model_id, q, (hipStream_t)stream);
+    }
+  } else {
+    e = amh::run_init(h->model_id, p, (hipStream_t)stream);
+  }
   if (e != hipSuccess) return hip_fail(h, e, "amh_init");
   return AMH_OK;
 }
@@ -183,6 +211,35 @@ int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_s
   p.gamma_tab = h->gamma_tab;
   p.gamma_tab_n = amh::kGammaTab;
   p.model = h->model;
+  if (amh::split_model(h->model_id, p.d)) {
+    // one transition = propose, batched potential, step(U(z') from memory);
+    // collection is per launch: step t keeps slot t / thinning when (t+1) % thinning == 0
+    const int64_t C = num_chains;
+    const size_t need = (size_t)C * (size_t)(p.d + 1) * sizeof(float);
+    int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_step/hipMalloc");
+    if (rc != AMH_OK) return rc;
+    float* xprop = h->split_buf;
+    float* peprop = h->split_buf + (size_t)C * p.d;
+    amh::StepParams q = p;
+    q.n_steps = 1;
+    q.thinning = 1;
+    q.ext_pe = peprop;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      q.in = (t == 0) ? *in : *out;
+      const bool keep = ((t + 1) % p.thinning) == 0;
+      const int64_t k = t / p.thinning;
+      q.col_z = (keep && p.col_z) ? p.col_z + (size_t)k * C * p.d : nullptr;
+      q.col_pe = (keep && p.col_pe) ? p.col_pe + (size_t)k * C : nullptr;
+      e = amh::run_propose(q, xprop, (hipStream_t)stream);
+      if (e == hipSuccess) {
+        amh::PotParams pp{xprop, peprop, C, p.d, h->model};
+        e = amh::run_potential_lane(h->model_id, pp, (hipStream_t)stream);
+      }
+      if (e == hipSuccess) e = amh::run_step_ext(q, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_step(split)");
+    }
+    return AMH_OK;
+  }
   e = amh::run_step(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_step");
   return AMH_OK;
@@ -195,7 +252,8 @@ int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* str
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential/hipSetDevice");
   amh::PotParams p{z, pe, n, h->cfg.dim, h->model};
-  e = amh::run_potential(h->model_id, p, (hipStream_t)stream);
+  e = amh::split_model(h->model_id, p.d) ? amh::run_potential_lane(h->model_id, p, (hipStream_t)stream)
+                                         : amh::run_potential(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential");
   return AMH_OK;
 }

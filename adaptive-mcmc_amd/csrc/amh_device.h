@@ -378,6 +378,23 @@ struct DiamondsM {
   }
 };
 
+// Potential evaluated outside the step kernel (split path, amh_split.hip):
+// the step kernel reads U(z') from StepParams::ext_pe instead of calling
+// potential(); init leaves pe for the batched potential kernel to fill.
+template <int G>
+struct ExtPotM {
+  struct Ctx {};
+  static constexpr bool kExternal = true;
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int) { return 0; }
+  static __device__ void stage(float*, const ModelArgs&, int) {}
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs&, int, int) { return Ctx{}; }
+  static __device__ __forceinline__ float potential(float, int, int, const Ctx&, const float*) { return 0.0f; }
+};
+template <class T, class = void>
+struct is_external : std::false_type {};
+template <class T>
+struct is_external<T, std::void_t<decltype(T::kExternal)>> : std::bool_constant<T::kExternal> {};
+
 // --------------------------------------------------------------- geometry --
 constexpr int kBlock = 256;       // 4 waves (init / potential / sample_Pnx kernels)
 constexpr int kBlockStep = 1024;  // 16 waves per CU share one staged copy of the model data

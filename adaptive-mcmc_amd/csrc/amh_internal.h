@@ -32,6 +32,7 @@ struct StepParams {
   const float* gamma_tab;  // gamma_n = amh_lr_gamma(n, a) for n < gamma_tab_n
   int32_t gamma_tab_n;
   ModelArgs model;
+  const float* ext_pe;     // split path: U(z') per chain from the batched potential (n_steps == 1)
 };
 
 struct InitParams {
@@ -98,6 +99,13 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
 hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);
+// split path for data-heavy models (diamonds): proposal kernel, lane-per-chain
+// batched potential, then the step kernel reading U(z') (amh_split.hip)
+bool split_model(int model_id, int d);
+hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s);
+hipError_t run_step_ext(const StepParams& p, hipStream_t s);
+hipError_t run_init_nopot(const InitParams& p, hipStream_t s);
+hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, uint32_t* out,
                           hipStream_t s);
 #ifdef AMH_STAMPS

@@ -80,7 +80,7 @@ __host__ __device__ __forceinline__ int wbuf_floats(int cpw, int d) {
 
 // Issue the DMA of one work item's chain state (global -> this wave's LDS
 // buffer).  Out-of-range bytes (past C) read as zero.
-template <int G>
+template <int G, bool EXT>
 __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first, int d, float* wb, int lane) {
   constexpr int CPW = Geo<G>::CPW;
   const uint32_t P = (uint32_t)(d * (d + 1) / 2);
@@ -133,6 +133,10 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
   if (lane < 2 * CPW) {
     const Buf bk(uniform_ptr(p.in.rng_key + 2 * first), (uint32_t)nvalid * 8u);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(bk.rs, to_lds(ws + 5 * CPW), 4, (int)(4u * lane), 0, 0, 0);
+  }
+  if (EXT && lane < CPW) {  // split path: U(z') of the batched potential kernel
+    const Buf be(uniform_ptr(p.ext_pe + first), (uint32_t)nvalid * 4u);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(be.rs, to_lds(ws + 7 * CPW), 4, (int)(4u * lane), 0, 0, 0);
   }
 }
 
@@ -205,6 +209,7 @@ template <int DMAX, template <int> class M, bool EXACT>
 __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   constexpr int G = DMAX;
   constexpr int CPW = Geo<G>::CPW;
+  constexpr bool kExt = is_external<M<G>>::value;
   using Gp = Grp<G>;
   extern __shared__ float lds[];
   const int d = EXACT ? DMAX : p.d;
@@ -231,6 +236,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   // issued after the wait, so the next wait never has to drain them.
   float U[DMAX];
   float dl = 0.0f, z = 0.0f, mu = 0.0f, pe = 0.0f, macc = 0.0f, lam = 0.0f, asc = 0.0f;
+  [[maybe_unused]] float pe_ext = 0.0f;  // split path: U(z') computed outside
   int32_t it = 0, nacc = 0, acc0 = 0;
   uint32_t k0 = 0, k1 = 0;
   bool updated = false;
@@ -322,7 +328,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   int64_t item = ticket();
   int64_t nxt = item < blk_hi ? ticket() : blk_hi;
 
-  if (item < blk_hi) prefetch_item<G>(p, item * CPW, d, wb, lane_id());
+  if (item < blk_hi) prefetch_item<G, kExt>(p, item * CPW, d, wb, lane_id());
   for (; item < blk_hi;) {
     // Every lane-dependent quantity is derived from an opaque copy of the lane
     // id inside the loop: otherwise the compiler hoists dozens of per-column
@@ -371,12 +377,13 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       asc = wsc[4 * CPW + g];
       k0 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g]);
       k1 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g + 1]);
+      if constexpr (kExt) pe_ext = wsc[7 * CPW + g];
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): buffer consumed before it is refilled
     AMH_STAMP(2)
     int64_t nxt2 = blk_hi;
     if (nxt < blk_hi) {
-      prefetch_item<G>(p, nxt * CPW, d, wb, lane);
+      prefetch_item<G, kExt>(p, nxt * CPW, d, wb, lane);
       nxt2 = ticket();
     }
     AMH_STAMP(3)
@@ -410,7 +417,12 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
 
       // ---- potential, NaN -> +inf (arwmh.py:169-171)
 #ifndef AMH_ABLATE_POT
-      float pep = M<G>::potential(zp, r, d, mctx, lds);
+      float pep;
+      if constexpr (kExt) {
+        pep = pe_ext;  // n_steps == 1 (host-enforced)
+      } else {
+        pep = M<G>::potential(zp, r, d, mctx, lds);
+      }
 #else
       float pep = Gp::sum(zp * zp);
 #endif
@@ -803,6 +815,17 @@ hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s) {
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s) {
   return dispatch(model_id, p.d, PnxF{p, s});
 }
+// split path (amh_split.hip): the step kernel with U(z') read from p.ext_pe,
+// and init without the potential (filled by the batched potential kernel)
+hipError_t run_step_ext(const StepParams& p, hipStream_t s) {
+  if (p.d < 1 || p.d > 32 || p.n_steps != 1 || p.ext_pe == nullptr) return hipErrorInvalidValue;
+  return launch_step<32, ExtPotM, false>(p, s);
+}
+hipError_t run_init_nopot(const InitParams& p, hipStream_t s) {
+  if (p.d < 1 || p.d > 32) return hipErrorInvalidValue;
+  return launch_init<32, ExtPotM, false>(p, s);
+}
+
 hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, uint32_t* out, hipStream_t s) {
   const int blocks = (int)((n + 255) / 256);
   hipLaunchKernelGGL(chain_keys_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, s, k0, k1, offset, n, out);

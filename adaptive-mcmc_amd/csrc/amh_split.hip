@@ -1,0 +1,194 @@
+// amh_split.hip -- the split transition for data-heavy models (diamonds).
+//
+// The fused step kernel evaluates the potential with the chain's lane group
+// (lane r sums rows n = r, r+G, ...), so every chain streams the whole data
+// set (diamonds: N x Kc = 5000 x 24 floats, 480 KB) through the cache per
+// step: 262,144 chains move 126 GB of L2 traffic per transition.  Here one
+// transition is three launches:
+//
+//   propose_kernel      z' = z + (L e^lam + eps I) xi   (arwmh.py:162-167)
+//   *_pot_lane_kernel   U(z'), ONE LANE PER CHAIN: the data rows arrive as
+//                       wave-uniform scalar loads shared by 64 chains, the
+//                       chain's coefficients sit in the lane's registers
+//                       (run_diamonds_lr_decay.py:24-40)
+//   step kernel (ExtPotM) accept / adaptation with U(z') read from memory
+//                       (arwmh.py:168-207), recomputing z' in registers
+//
+// Bit spec: the proposal is the step kernel's expression, evaluated in the
+// same order (so the step kernel's recomputed z' is the one evaluated here),
+// and the lane kernel keeps the group kernel's summation order -- 32 partial
+// sums over rows n = r (mod 32), each in row order, then the group's xor
+// butterfly (oracle: pot_diamonds, group_sum).  The split path is therefore
+// bit-identical to the fused one (tests/test_gpu_parity.py).
+#include "amh_device.h"
+
+namespace amh {
+
+bool split_model(int model_id, int d) { return model_id == AMH_MODEL_DIAMONDS && d >= 3 && d <= 32; }
+
+// ---------------------------------------------------------------- propose --
+// Lane group of G = 32 per chain, lane r = row r; the factor is read straight
+// from HBM (each column of a chain is one coalesced access).  U_rj and the
+// four partial sums follow arwmh_step_kernel exactly.
+template <int G>
+__global__ __launch_bounds__(kBlock) void propose_kernel(StepParams p, float* __restrict__ xprop) {
+  using Gp = Grp<G>;
+  const int d = p.d;
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.C;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
+  const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
+  for (int64_t item = wave0; item < n_items; item += wstride) {
+    const int64_t chain = item_chain<G>(item);
+    const bool chain_ok = chain < C;
+    const int64_t cl = chain_ok ? chain : C - 1;
+    const float* Lc = p.in.scale + cl * P;
+    const float dl = act ? Lc[col_off(d, r)] : 0.0f;
+    const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+    float U[G];
+    static_for<G>([&](auto J) {
+      constexpr int j = J;
+      U[j] = 0.0f;
+      if (j < d) {
+        const float x = (act && r > j) ? Lc[col_off(d, j) + (r - j)] : 0.0f;
+        const float ij = Gp::template bcast<j>(inv);
+        U[j] = (r == j) ? 1.0f : ((r > j) ? x * ij : 0.0f);
+      }
+    });
+    const int32_t it = p.in.i[cl];
+    const uint32_t k0 = p.in.rng_key[2 * cl], k1 = p.in.rng_key[2 * cl + 1];
+    const float z = act ? p.in.z[cl * d + r] : 0.0f;
+    const float lam = p.in.log_step_size[cl];
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+    const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+    const float el = amh_expf(lam);
+    const float eta = dl * xi;
+    float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    static_for<G>([&](auto J) {
+      if (J < d) a4[J & 3] = fmaf(U[J], Gp::template bcast<J>(eta), a4[J & 3]);
+    });
+    const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+    const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+    if (chain_ok && act) xprop[chain * d + r] = zp;
+  }
+}
+
+// ------------------------------------------------ diamonds, lane per chain --
+// xor butterfly of the G = 32 group (Grp<32>::sum / oracle group_sum) on 32
+// values held by one lane
+__device__ __forceinline__ float butterfly32(float (&x)[32]) {
+  static_for<5>([&](auto S) {
+    constexpr int off = 1 << S;
+    float y[32];
+    static_for<32>([&](auto R) { y[R] = x[R] + x[R ^ off]; });
+    static_for<32>([&](auto R) { x[R] = y[R]; });
+  });
+  return x[0];
+}
+
+typedef __attribute__((address_space(4))) const float cfloat;
+
+// z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)].  KC > 0:
+// compile-time Kc (the reference data set: K = 25); KC == 0: any Kc <= 30.
+template <int KC>
+__global__ __launch_bounds__(256) void diamonds_pot_lane_kernel(PotParams p) {
+  constexpr int KMAX = KC > 0 ? KC : 30;
+  const int Kc = KC > 0 ? KC : (int)p.model.k - 1;
+  const int d = p.d;
+  const int64_t N = p.model.n;
+  const int64_t n_ch = p.n;
+  int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool ok = c < n_ch;
+  if (!ok) c = n_ch - 1;
+  const float* zc = p.z + c * d;
+  float b[KMAX];
+  static_for<KMAX>([&](auto K) { b[K] = (K < Kc) ? zc[1 + K] : 0.0f; });
+  const float icpt = zc[0];
+  const float ls = zc[Kc + 1];
+  const float sg = amh_expf(ls);
+  const float isg = 1.0f / sg;
+  const cfloat* X = (const cfloat*)p.model.data;
+  const cfloat* Y = X + N * Kc;
+  float part[32];
+  static_for<32>([&](auto R) { part[R] = 0.0f; });
+  auto row = [&](const float (&xr)[KMAX], float yn, float& acc) {
+    float mu = 0.0f;
+    static_for<KMAX>([&](auto K) {
+      if (K < Kc) mu = fmaf(xr[K], b[K], mu);
+    });
+    const float e = (yn - (icpt + mu)) * isg;
+    acc = fmaf(e, e, acc);
+  };
+  auto load = [&](int64_t n, float (&xr)[KMAX], float& yn) {
+    static_for<KMAX>([&](auto K) { xr[K] = (K < Kc) ? X[n * Kc + K] : 0.0f; });
+    yn = Y[n];
+  };
+  // whole blocks of 32 rows: row n+1's scalar loads are issued before row n's
+  // FMAs, so the wave waits on the scalar cache once per row at most
+  const int64_t Nfull = N & ~(int64_t)31;
+  if (Nfull > 0) {
+    float cur[KMAX], ycur;
+    load(0, cur, ycur);
+    for (int64_t n0 = 0; n0 < Nfull; n0 += 32) {
+      static_for<32>([&](auto R) {
+        float nxt[KMAX], ynxt;
+        const int64_t nn = (n0 + R + 1 < Nfull) ? n0 + R + 1 : n0 + R;
+        load(nn, nxt, ynxt);
+        row(cur, ycur, part[R]);
+        static_for<KMAX>([&](auto K) { cur[K] = nxt[K]; });
+        ycur = ynxt;
+      });
+    }
+  }
+  static_for<32>([&](auto R) {  // ragged tail: rows Nfull .. N-1
+    const int64_t n = Nfull + R;
+    if (n < N) {
+      float xr[KMAX], yn;
+      load(n, xr, yn);
+      row(xr, yn, part[R]);
+    }
+  });
+  const float S = butterfly32(part);
+  float bb[32];  // group lane r holds coordinate r: b_{r-1}^2 for 1 <= r <= Kc
+  static_for<32>([&](auto R) {
+    constexpr int r = R;
+    if constexpr (r >= 1 && r - 1 < KMAX) {
+      bb[r] = (r <= Kc) ? b[r - 1] * b[r - 1] : 0.0f;
+    } else {
+      bb[r] = 0.0f;
+    }
+  });
+  const float B = butterfly32(bb);
+  const float cst = -3.30347394261755545f;
+  const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+  const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+  const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+  const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+  if (ok) p.pe[c] = -(((ll + lpb) + lpi) + lps);
+}
+
+// ---------------------------------------------------------------- launchers --
+hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
+  if (p.d < 1 || p.d > 32) return hipErrorInvalidValue;
+  const int64_t n_items = (p.C + Geo<32>::CPW - 1) / Geo<32>::CPW;
+  int64_t blocks = (n_items + kBlock / 64 - 1) / (kBlock / 64);
+  if (blocks > 256 * 32) blocks = 256 * 32;
+  hipLaunchKernelGGL(propose_kernel<32>, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s, p, xprop);
+  return hipGetLastError();
+}
+
+hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s) {
+  if (!split_model(model_id, p.d)) return hipErrorInvalidValue;
+  const int64_t blocks = (p.n + 255) / 256;
+  if (p.model.k - 1 == 24) {
+    hipLaunchKernelGGL(diamonds_pot_lane_kernel<24>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  } else {
+    hipLaunchKernelGGL(diamonds_pot_lane_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace amh

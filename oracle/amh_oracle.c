@@ -52,6 +52,14 @@ int orc_group_width(int d) {
   return g;
 }
 
+/* Group width of the per-chain kernels for a model (amh_device.h dispatch):
+ * eight schools runs at G = 16 and diamonds at G = 32 for every d they take. */
+static int orc_gw(const orc_cfg* cfg) {
+  if (cfg->model_id == ORC_DIAMONDS) return 32;
+  if (cfg->model_id == ORC_EIGHT_SCHOOLS) return 16;
+  return orc_group_width(cfg->d);
+}
+
 /* ----------------------------------------------------- lane-group ops ---- */
 /* butterfly sum: for off = 1,2,4,..: x[r] = x[r] + x[r ^ off] */
 static float group_sum(const float* in, int G) {
@@ -217,7 +225,7 @@ static float pot_diamonds(const orc_cfg* cfg, const float* x, int G) {
 }
 
 float orc_potential1(const orc_cfg* cfg, const float* x) {
-  const int G = orc_group_width(cfg->d);
+  const int G = orc_gw(cfg);
   switch (cfg->model_id) {
     case ORC_GAUSSIAN: return pot_gaussian(cfg, x, G);
     case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
@@ -290,7 +298,7 @@ typedef struct {
 /* One ARWMH transition of one chain (arwmh.py:140-207). Returns accept. */
 static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, uint32_t ctr) {
   const int d = cfg->d;
-  const int G = orc_group_width(d);
+  const int G = orc_gw(cfg);
   /* arwmh.py:162-165: proposal noise and accept uniform */
   float xi[ORC_DMAX];
   uint32_t ubits = 0;
@@ -462,12 +470,17 @@ void orc_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float
 #pragma omp parallel for schedule(dynamic, 16)
   for (int64_t c = 0; c < C; ++c) {
     chain_t* s = (chain_t*)malloc(sizeof(chain_t));
+    /* the split transition (data-heavy models, amh_split.hip) is one launch
+     * per step: the state goes through HBM (L = U diag(dl)) between steps */
+    const int split = cfg->model_id == ORC_DIAMONDS && d >= 3 && d <= 32;
     chain_load(cfg, s, c, i_, z, pe, macc, mu, L, lam, asc);
     int nacc = 0;
     for (int32_t t = 0; t < n_steps; ++t) {
+      if (split && t > 0) chain_load(cfg, s, c, i_, z, pe, macc, mu, L, lam, asc);
       nacc += chain_step(cfg, s, keys[2 * c], keys[2 * c + 1], (uint32_t)s->i);
       if (collect_z)
         for (int r = 0; r < d; ++r) collect_z[((int64_t)t * C + c) * d + r] = s->z[r];
+      if (split && t + 1 < n_steps) chain_store(cfg, s, c, L, i_, z, pe, macc, mu, L, lam, asc);
     }
     chain_store(cfg, s, c, L, i_, z, pe, macc, mu, L, lam, asc);
     if (accept_count) accept_count[c] += nacc;

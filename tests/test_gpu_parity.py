@@ -57,7 +57,8 @@ def test_single_steps_bitexact(kind, d, C, gpu, orc):
     np.testing.assert_array_equal(k.accept_count.cpu().numpy(), acc)
 
 
-@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 2000), ("eight_schools", None, 1000)])
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 2000), ("eight_schools", None, 1000),
+                                      ("diamonds", None, 130)])
 def test_fused_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.run (n steps in one launch, z collected) vs oracle step(n_steps)."""
     k, st, om, ost = _init(kind, C, gpu, orc, d=d)
@@ -80,6 +81,32 @@ def test_inplace_and_thinning(gpu, orc):
     k.sample_(st2, 5)
     orc.step(om, ost, 5)
     assert_state_bitequal(st2, ost, "in-place")
+
+
+def test_split_path_generic_k(gpu, orc):
+    """Diamonds through the split transition (propose / lane-per-chain
+    potential / step) with a data shape off the compile-time fast path
+    (K = 10, ragged N = 77): collection with thinning and in-place steps
+    stay bit-identical to the oracle."""
+    import posteriors as P
+    from kernels import ARWMH, PRNGKey
+    mk = P.synthetic_diamonds(N=77, K=10, seed=5)
+    arr, (N, K) = P.diamonds.pack_fn(mk)
+    om = orc.Model(orc.DIAMONDS, K + 1, arr, n_data=N, k_data=K)
+    C = 199
+    k = ARWMH(model=P.diamonds, num_chains=C)
+    st = k.init(PRNGKey(4), 5, None, (), mk)
+    ost = orc.init(om, PRNGKey(4), C)
+    assert_state_bitequal(st, ost, "split init")
+    st2, cz, cp = k.run(st, 12, thinning=4, collect_z=True, collect_pe=True)
+    ocz = orc.step(om, ost, 12, num_warmup=5, collect_z=True)
+    np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), ocz[3::4].view(np.uint32))
+    k.sample_(st2, 3)
+    orc.step(om, ost, 3, num_warmup=5)
+    assert_state_bitequal(st2, ost, "split in-place")
+    z = np.random.default_rng(2).normal(size=(300, K + 1)).astype(np.float32)
+    pe = k.potential(torch.as_tensor(z, device=gpu)).cpu().numpy()
+    np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
 
 
 def test_sample_pnx_bitexact(gpu, orc):
