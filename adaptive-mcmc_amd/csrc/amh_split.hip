@@ -93,14 +93,27 @@ typedef __attribute__((address_space(4))) const float cfloat;
 
 // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)].  KC > 0:
 // compile-time Kc (the reference data set: K = 25); KC == 0: any Kc <= 30.
+//
+// A block of 4 waves serves 64 chains (lane l = chain 64 * block + l).  The
+// 32 partial sums of the bit spec are independent FMA chains (rows n = r mod
+// 32, each in row order), so wave w owns residues r in [8w, 8w + 8) and reads
+// only those rows: 4x the waves per chain (the scalar-load latency of one
+// row is hidden by the other waves of the SIMD) at unchanged bits.  The 32
+// partials then meet in LDS and wave 0 finishes the chain.
+constexpr int kDiaWaves = 4;
+constexpr int kDiaRes = 32 / kDiaWaves;  // residues per wave
+
 template <int KC>
-__global__ __launch_bounds__(256) void diamonds_pot_lane_kernel(PotParams p) {
+__global__ __launch_bounds__(64 * kDiaWaves) void diamonds_pot_lane_kernel(PotParams p) {
   constexpr int KMAX = KC > 0 ? KC : 30;
+  __shared__ float pl[32][64];
   const int Kc = KC > 0 ? KC : (int)p.model.k - 1;
   const int d = p.d;
   const int64_t N = p.model.n;
   const int64_t n_ch = p.n;
-  int64_t c = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  int64_t c = (int64_t)blockIdx.x * 64 + lane;
   const bool ok = c < n_ch;
   if (!ok) c = n_ch - 1;
   const float* zc = p.z + c * d;
@@ -112,8 +125,8 @@ __global__ __launch_bounds__(256) void diamonds_pot_lane_kernel(PotParams p) {
   const float isg = 1.0f / sg;
   const cfloat* X = (const cfloat*)p.model.data;
   const cfloat* Y = X + N * Kc;
-  float part[32];
-  static_for<32>([&](auto R) { part[R] = 0.0f; });
+  float part[kDiaRes];
+  static_for<kDiaRes>([&](auto Q) { part[Q] = 0.0f; });
   auto row = [&](const float (&xr)[KMAX], float yn, float& acc) {
     float mu = 0.0f;
     static_for<KMAX>([&](auto K) {
@@ -126,32 +139,43 @@ __global__ __launch_bounds__(256) void diamonds_pot_lane_kernel(PotParams p) {
     static_for<KMAX>([&](auto K) { xr[K] = (K < Kc) ? X[n * Kc + K] : 0.0f; });
     yn = Y[n];
   };
-  // whole blocks of 32 rows: row n+1's scalar loads are issued before row n's
-  // FMAs, so the wave waits on the scalar cache once per row at most
-  const int64_t Nfull = N & ~(int64_t)31;
-  if (Nfull > 0) {
+  // whole blocks of 32 rows: the next row's scalar loads are issued before
+  // this row's FMAs
+  const int64_t Mfull = N / 32;
+  const int64_t r0 = kDiaRes * w;
+  if (Mfull > 0) {
     float cur[KMAX], ycur;
-    load(0, cur, ycur);
-    for (int64_t n0 = 0; n0 < Nfull; n0 += 32) {
-      static_for<32>([&](auto R) {
+    load(r0, cur, ycur);
+    for (int64_t m = 0; m < Mfull; ++m) {
+      static_for<kDiaRes>([&](auto Q) {
         float nxt[KMAX], ynxt;
-        const int64_t nn = (n0 + R + 1 < Nfull) ? n0 + R + 1 : n0 + R;
+        int64_t nn;
+        if constexpr (Q + 1 < kDiaRes) {
+          nn = 32 * m + r0 + Q + 1;
+        } else {
+          nn = (m + 1 < Mfull) ? 32 * (m + 1) + r0 : 32 * m + r0 + Q;
+        }
         load(nn, nxt, ynxt);
-        row(cur, ycur, part[R]);
+        row(cur, ycur, part[Q]);
         static_for<KMAX>([&](auto K) { cur[K] = nxt[K]; });
         ycur = ynxt;
       });
     }
   }
-  static_for<32>([&](auto R) {  // ragged tail: rows Nfull .. N-1
-    const int64_t n = Nfull + R;
+  static_for<kDiaRes>([&](auto Q) {  // ragged tail: rows 32 Mfull .. N-1
+    const int64_t n = 32 * Mfull + r0 + Q;
     if (n < N) {
       float xr[KMAX], yn;
       load(n, xr, yn);
-      row(xr, yn, part[R]);
+      row(xr, yn, part[Q]);
     }
   });
-  const float S = butterfly32(part);
+  static_for<kDiaRes>([&](auto Q) { pl[r0 + Q][lane] = part[Q]; });
+  __syncthreads();
+  if (w != 0) return;
+  float all[32];
+  static_for<32>([&](auto R) { all[R] = pl[R][lane]; });
+  const float S = butterfly32(all);
   float bb[32];  // group lane r holds coordinate r: b_{r-1}^2 for 1 <= r <= Kc
   static_for<32>([&](auto R) {
     constexpr int r = R;
@@ -182,11 +206,11 @@ hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
 
 hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s) {
   if (!split_model(model_id, p.d)) return hipErrorInvalidValue;
-  const int64_t blocks = (p.n + 255) / 256;
+  const int64_t blocks = (p.n + 63) / 64;
   if (p.model.k - 1 == 24) {
-    hipLaunchKernelGGL(diamonds_pot_lane_kernel<24>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(diamonds_pot_lane_kernel<24>, dim3((unsigned)blocks), dim3(64 * kDiaWaves), 0, s, p);
   } else {
-    hipLaunchKernelGGL(diamonds_pot_lane_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(diamonds_pot_lane_kernel<0>, dim3((unsigned)blocks), dim3(64 * kDiaWaves), 0, s, p);
   }
   return hipGetLastError();
 }
