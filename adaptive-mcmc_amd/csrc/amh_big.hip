@@ -1,0 +1,432 @@
+// amh_big.hip -- ARWMH for large dimensions (64 < d <= 256, d % 32 == 0,
+// dense Gaussian potential; BASELINE config 4: d = 256, kappa = 1e4).
+//
+// At d = 256 a chain's packed factor is 131.6 KB: it cannot live in one
+// wave's registers, and the dense precision (256 KB) cannot sit in LDS next
+// to anything else.  One transition is therefore three launches:
+//
+//   big_propose_kernel   one wave per chain, lane l owns rows 64 s + l.  One
+//                        pass over the factor in column order computes the
+//                        proposal z' = z + (L e^lam + eps I) xi (arwmh.py:
+//                        166-167) and, because row r's proposal is complete
+//                        once column r has passed, BOTH forward solves of the
+//                        rank-one update (w = U^-1 delta for the accepted and
+//                        for the rejected delta) in the same pass.
+//   gauss_pot_mfma_kernel U(z') for 64 chains per block on MFMA
+//                        (v_mfma_f32_32x32x2_f32: Y = P D, D = z' - m; the
+//                        f32 MFMA is a k-ordered fmaf chain, so the oracle
+//                        can mirror it bit for bit).  Shared by init and
+//                        amh_potential.
+//   big_step_kernel      one wave per chain: accept (arwmh.py:173-178), the
+//                        schedule and mean / step-size updates (:180-193) and
+//                        the second pass over the factor, which applies the
+//                        rank-one update column by column and streams L' out
+//                        (cholesky_update at :190, keep-L rule at :191).
+//
+// The factor is read twice and written once per transition (the algorithmic
+// count is one read and one write); the passes stream it with coalesced
+// column accesses and keep nothing but O(d) per chain on chip.
+// Bit spec: oracle/amh_oracle.c, "large dimensions".
+#include "amh_device.h"
+
+namespace amh {
+
+namespace {
+
+constexpr int kNS = 4;  // row slots per lane: d <= 64 * kNS
+
+__device__ __forceinline__ float rdl(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+
+// gamma_n (scalar cache table, as the step kernel)
+__device__ __forceinline__ float big_gamma(const BigParams& p, int32_t n) {
+  typedef __attribute__((address_space(4))) const float cf;
+  const cf* tab = (const cf*)p.gamma_tab;
+  return (n < p.gamma_tab_n) ? tab[n] : amh_lr_gamma(n, p.a);
+}
+
+// sum over rows: 64-lane butterfly per slot, then (s0 + s1) + (s2 + s3)
+__device__ __forceinline__ float big_sum(const float (&v)[kNS]) {
+  float s[kNS];
+  static_for<kNS>([&](auto K) { s[K] = Grp<64>::sum(v[K]); });
+  return (s[0] + s[1]) + (s[2] + s[3]);
+}
+
+}  // namespace
+
+// --------------------------------------------------------------- init ----
+// arwmh.py:84-138 (init_to_uniform), one wave per chain; pe0 is filled by
+// the MFMA potential afterwards.
+__global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
+  const int d = p.d;
+  const int lane = lane_id();
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
+    const uint64_t gc = (uint64_t)(p.chain_offset + c);
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)gc, (uint32_t)(gc >> 32), 0u, AMH_TAG_CHAINKEY, p.key0, p.key1);
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) {
+        float z0;
+        if (p.init_z != nullptr) {
+          z0 = p.init_z[c * d + r];
+        } else {
+          const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, 0u, 0u, AMH_TAG_INIT, kk.v[0], kk.v[1]);
+          const float v = (amh_unif01_from_bits(o.v[0]) * 4.0f) + (-2.0f);
+          z0 = (v < -2.0f) ? -2.0f : v;
+        }
+        p.out.z[c * d + r] = z0;
+        p.out.loc[c * d + r] = z0;
+      }
+    });
+    float* Lc = p.out.scale + c * P;
+    for (int j = 0; j < d; ++j) {
+      static_for<kNS>([&](auto K) {
+        const int r = 64 * K + lane;
+        if (r >= j && r < d) Lc[col_off(d, j) + (r - j)] = (r == j) ? 1.0f : 0.0f;
+      });
+    }
+    if (lane == 0) {
+      p.out.i[c] = 0;
+      p.out.potential_energy[c] = 0.0f;
+      p.out.mean_accept_prob[c] = 0.0f;
+      p.out.log_step_size[c] = 0.0f;
+      p.out.as_change[c] = 0.0f;
+      p.out.rng_key[2 * c] = kk.v[0];
+      p.out.rng_key[2 * c + 1] = kk.v[1];
+    }
+  }
+}
+
+// ------------------------------------------------------------- propose ----
+__global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
+  const int d = p.d;
+  const int lane = lane_id();
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
+    const float* Lc = p.in.scale + c * P;
+    const int32_t it = p.in.i[c];
+    const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
+    const float el = amh_expf(p.in.log_step_size[c]);
+    float inv[kNS], xi[kNS], eta[kNS], zz[kNS], mu[kNS], acc[kNS], sa[kNS], sr[kNS], zp[kNS], wa[kNS], wr[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      const float dl = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
+      inv[K] = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+      xi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+      eta[K] = dl * xi[K];
+      zz[K] = act ? p.in.z[c * d + r] : 0.0f;
+      mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
+      acc[K] = sa[K] = sr[K] = zp[K] = wa[K] = wr[K] = 0.0f;
+    });
+    static_for<kNS>([&](auto KB) {
+      constexpr int kb = KB;
+      for (int jl = 0; jl < 64; ++jl) {
+        const int j = 64 * kb + jl;
+        if (j >= d) break;
+        const float etaj = rdl(eta[kb], jl);
+        const float invj = rdl(inv[kb], jl);
+        // row j completes its proposal and both solves at its own column
+        if (lane == jl) {
+          acc[kb] = fmaf(1.0f, etaj, acc[kb]);
+          zp[kb] = zz[kb] + fmaf(el, acc[kb], p.eps * xi[kb]);
+          wa[kb] = (zp[kb] - mu[kb]) - sa[kb];
+          wr[kb] = (zz[kb] - mu[kb]) - sr[kb];
+        }
+        const float waj = rdl(wa[kb], jl);
+        const float wrj = rdl(wr[kb], jl);
+        const float* col = Lc + col_off(d, j) - j;  // col[r] = L_rj
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r > j && r < d) {
+              const float uo = col[r] * invj;
+              acc[K] = fmaf(uo, etaj, acc[K]);
+              sa[K] = fmaf(uo, waj, sa[K]);
+              sr[K] = fmaf(uo, wrj, sr[K]);
+            }
+          }
+        });
+      }
+    });
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) {
+        p.xprop[c * d + r] = zp[K];
+        p.wa[c * d + r] = wa[K];
+        p.wr[c * d + r] = wr[K];
+      }
+    });
+  }
+}
+
+// ---------------------------------------------------------------- step ----
+__global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
+  const int d = p.d;
+  const int lane = lane_id();
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
+    const float* Lin = p.in.scale + c * P;
+    float* Lout = p.out.scale + c * P;
+    const int32_t it = p.in.i[c];
+    const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
+    const float pe = p.in.potential_energy[c];
+    const float macc = p.in.mean_accept_prob[c];
+    const float lam = p.in.log_step_size[c];
+    float pep = p.pep[c];
+    const float u = amh_unif01_from_bits(amh_philox4x32_10(0u, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1).v[1]);
+    if (amh_isnan(pep)) pep = INFINITY;
+    const float ex = amh_expf(pe - pep);
+    const float alpha = (ex > 1.0f) ? 1.0f : ex;
+    const bool accept = u < alpha;
+    const int32_t itr = it + 1;
+    const int32_t n = (it < p.W) ? itr : itr - p.W;
+    const float gamma = big_gamma(p, n);
+    const float maccn = macc + (alpha - macc) / (float)n;
+    const float lamn = lam + gamma * (alpha - p.target);
+    const float e1 = amh_expf(lamn);
+    const float el = amh_expf(lam);
+    const float sq = sqrtf(1.0f - gamma);
+    float dl[kNS], inv[kNS], zn[kNS], delta[kNS], mun[kNS], ws[kNS], Dg[kNS], one[kNS], gw2[kNS], t[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      dl[K] = act ? Lin[col_off(d, act ? r : 0)] : 0.0f;
+      inv[K] = (amh_isfinite(dl[K]) && dl[K] != 0.0f) ? 1.0f / dl[K] : 0.0f;
+      const float z = act ? p.in.z[c * d + r] : 0.0f;
+      const float mu = act ? p.in.loc[c * d + r] : 0.0f;
+      const float zpv = act ? p.xprop[c * d + r] : 0.0f;
+      const float w = act ? (accept ? p.wa[c * d + r] : p.wr[c * d + r]) : 0.0f;
+      zn[K] = accept ? zpv : z;
+      delta[K] = act ? zn[K] - mu : 0.0f;
+      mun[K] = act ? mu + gamma * delta[K] : 0.0f;
+      ws[K] = w;
+      const float ajj = sq * dl[K];
+      Dg[K] = ajj * ajj;
+      one[K] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+      gw2[K] = act ? gamma * (w * w) : 0.0f;
+      t[K] = act ? gw2[K] / Dg[K] : 0.0f;
+    });
+    // b_j: 64-lane exclusive scan per slot plus the carry of the slots before
+    float cc[kNS], qq[kNS];
+    bool bad = false;
+    float carry = 0.0f;
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      const float e = Grp<64>::excl_scan(t[K], lane);
+      const float bs = (K == 0) ? e : e + carry;
+      const float tot = rdl(e + t[K], 63);
+      carry = (K == 0) ? tot : carry + tot;
+      const float b = 1.0f + bs;
+      const float g2 = (b * Dg[K]) + gw2[K];
+      const float dn = g2 / b;
+      cc[K] = (gamma * ws[K]) / g2;
+      qq[K] = sqrtf(dn);
+      const float dnew = fmaf(cc[K], 0.0f, one[K]) * qq[K];
+      bad = bad || (act && amh_isnan(dnew));
+    });
+    const bool revert = __ballot(bad) != 0ull;
+    float sacc[kNS];
+    static_for<kNS>([&](auto K) { sacc[K] = 0.0f; });
+    if (!revert) {
+      float ac[kNS], bc[kNS], sv[kNS];
+      static_for<kNS>([&](auto K) {
+        ac[K] = (qq[K] * e1) - (dl[K] * el);
+        bc[K] = (cc[K] * qq[K]) * e1;
+        sv[K] = 0.0f;
+      });
+      static_for<kNS>([&](auto KB) {
+        constexpr int kb = KB;
+        for (int jl = 0; jl < 64; ++jl) {
+          const int j = 64 * kb + jl;
+          if (j >= d) break;
+          const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
+          const float bcj = rdl(bc[kb], jl), invj = rdl(inv[kb], jl), qj = rdl(qq[kb], jl);
+          const float* col = Lin + col_off(d, j) - j;
+          float* ocol = Lout + col_off(d, j) - j;
+          if (lane == jl) {
+            const float tt = fmaf(1.0f, acj, bcj * 0.0f);
+            sacc[kb] = fmaf(tt, tt, sacc[kb]);
+            ocol[j] = 1.0f * qj;
+          }
+          static_for<kNS>([&](auto K) {
+            if constexpr (K >= kb) {
+              const int r = 64 * K + lane;
+              if (r > j && r < d) {
+                const float uo = col[r] * invj;
+                sv[K] = fmaf(uo, wsj, sv[K]);
+                const float w = delta[K] - sv[K];
+                const float un = fmaf(cj, w, uo);
+                const float tt = fmaf(uo, acj, bcj * w);
+                sacc[K] = fmaf(tt, tt, sacc[K]);
+                ocol[r] = un * qj;
+              }
+            }
+          });
+        }
+      });
+    } else {
+      // factor kept (arwmh.py:191): copied verbatim; as_change = ||L (e1 - e0)||_F
+      float ac[kNS];
+      static_for<kNS>([&](auto K) { ac[K] = (dl[K] * e1) - (dl[K] * el); });
+      static_for<kNS>([&](auto KB) {
+        constexpr int kb = KB;
+        for (int jl = 0; jl < 64; ++jl) {
+          const int j = 64 * kb + jl;
+          if (j >= d) break;
+          const float acj = rdl(ac[kb], jl), invj = rdl(inv[kb], jl);
+          const float* col = Lin + col_off(d, j) - j;
+          float* ocol = Lout + col_off(d, j) - j;
+          if (lane == jl) {
+            const float t0 = 1.0f * acj;
+            sacc[kb] = fmaf(t0, t0, sacc[kb]);
+            ocol[j] = dl[kb];
+          }
+          static_for<kNS>([&](auto K) {
+            if constexpr (K >= kb) {
+              const int r = 64 * K + lane;
+              if (r > j && r < d) {
+                const float x = col[r];
+                const float tt = (x * invj) * acj;
+                sacc[K] = fmaf(tt, tt, sacc[K]);
+                ocol[r] = x;
+              }
+            }
+          });
+        }
+      });
+    }
+    const float asc = sqrtf(big_sum(sacc));
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) {
+        p.out.z[c * d + r] = zn[K];
+        p.out.loc[c * d + r] = mun[K];
+        if (p.col_z != nullptr) p.col_z[c * d + r] = zn[K];
+      }
+    });
+    if (lane == 0) {
+      p.out.i[c] = itr;
+      p.out.potential_energy[c] = accept ? pep : pe;
+      p.out.mean_accept_prob[c] = maccn;
+      p.out.log_step_size[c] = lamn;
+      p.out.as_change[c] = asc;
+      p.out.rng_key[2 * c] = k0;
+      p.out.rng_key[2 * c + 1] = k1;
+      if (p.accept_count != nullptr) p.accept_count[c] += accept ? 1 : 0;
+      if (p.col_pe != nullptr) p.col_pe[c] = accept ? pep : pe;
+    }
+  }
+}
+
+// ------------------------------------------------- potential on MFMA ----
+// 64 chains per block (two 32-chain tiles), 4 waves; wave w owns the 32-row
+// tiles 2w and 2w + 1.  D = z' - m is staged k-major in LDS ([k][chain],
+// rows padded to 65 floats); A = P rows straight from L2.
+constexpr int kPotChains = 64;
+constexpr int kPotLd = 65;
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__host__ __device__ inline size_t pot_mfma_lds(int d) { return ((size_t)d * kPotLd + 8 * kPotChains) * sizeof(float); }
+
+__global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
+  extern __shared__ float lds_pot[];
+  const int d = p.d;
+  float* Dt = lds_pot;
+  float(*tsum)[kPotChains] = (float(*)[kPotChains])(lds_pot + (size_t)d * kPotLd);
+  const int nt = d / 32;
+  const float* m = p.model.data;
+  const float* Pm = p.model.data + d;
+  const float c0 = p.model.data[d + d * d];
+  const int64_t cbase = (int64_t)blockIdx.x * kPotChains;
+  for (int idx = threadIdx.x; idx < kPotChains * d; idx += 256) {
+    const int cc = idx / d, k = idx - cc * d;
+    int64_t ch = cbase + cc;
+    if (ch >= p.n) ch = p.n - 1;
+    Dt[k * kPotLd + cc] = p.z[ch * d + k] - m[k];
+  }
+  __syncthreads();
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  const int h = lane >> 5, i = lane & 31;
+  f32x16 acc[2][2];
+  static_for<2>([&](auto I) { static_for<2>([&](auto T) { acc[I][T] = f32x16{}; }); });
+  const bool has1 = 2 * w + 1 < nt;
+  const bool has0 = 2 * w < nt;
+  const float* prow0 = Pm + (int64_t)(32 * (2 * w) + i) * d;
+  const float* prow1 = Pm + (int64_t)(32 * (2 * w + 1) + i) * d;
+  if (has0) {
+    for (int kk = 0; kk < d; kk += 2) {
+      const float b0 = Dt[(kk + h) * kPotLd + i];
+      const float b1 = Dt[(kk + h) * kPotLd + 32 + i];
+      const float a0 = prow0[kk + h];
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+      if (has1) {
+        const float a1 = prow1[kk + h];
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+      }
+    }
+  }
+  // q = D_r y_r summed over the accumulator layout, then the two lane halves
+  static_for<2>([&](auto I) {
+    const int tile = 2 * w + I;
+    if (tile < nt) {
+      static_for<2>([&](auto T) {
+        float ps = 0.0f;
+        static_for<16>([&](auto R) {
+          const int row = 32 * tile + (R & 3) + 8 * (R >> 2) + 4 * h;
+          ps = ps + Dt[row * kPotLd + 32 * T + i] * acc[I][T][(int)R];
+        });
+        const float other = __shfl_xor(ps, 32, 64);
+        const float tI = (h == 0) ? ps + other : other + ps;
+        if (h == 0) tsum[tile][32 * T + i] = tI;
+      });
+    }
+  });
+  __syncthreads();
+  if (w == 0) {
+    float S = 0.0f;
+    for (int t = 0; t < nt; ++t) S = S + tsum[t][lane];
+    const int64_t ch = cbase + lane;
+    if (ch < p.n) p.pe[ch] = (0.5f * S) + c0;
+  }
+}
+
+// ------------------------------------------------------------- launchers ----
+bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256 && d % 32 == 0; }
+
+static int wave_grid(int64_t n) {
+  int64_t b = (n + 3) / 4;
+  if (b > 256 * 16) b = 256 * 16;
+  return (int)(b > 0 ? b : 1);
+}
+
+hipError_t run_big_init(const InitParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(big_init_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(big_propose_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t run_big_step(const BigParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(big_step_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  return hipGetLastError();
+}
+hipError_t run_big_potential(const PotParams& p, hipStream_t s) {
+  const int64_t blocks = (p.n + kPotChains - 1) / kPotChains;
+  hipLaunchKernelGGL(gauss_pot_mfma_kernel, dim3((unsigned)blocks), dim3(256), pot_mfma_lds(p.d), s, p);
+  return hipGetLastError();
+}
+
+}  // namespace amh

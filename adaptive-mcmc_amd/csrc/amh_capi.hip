@@ -100,7 +100,7 @@ const char* amh_last_error(const amh_handle* h) { return h ? h->err.c_str() : g_
 
 int amh_create(const amh_config* cfg, int device, amh_handle** out) {
   if (!cfg || !out) return fail(nullptr, AMH_EINVAL, "amh_create: null argument");
-  if (cfg->dim < 1 || cfg->dim > 64) return fail(nullptr, AMH_EINVAL, "amh_create: dim must be in [1, 64]");
+  if (cfg->dim < 1 || cfg->dim > 256) return fail(nullptr, AMH_EINVAL, "amh_create: dim must be in [1, 256]");
   if (cfg->num_warmup < 0) return fail(nullptr, AMH_EINVAL, "amh_create: num_warmup < 0");
   amh_handle* h = new (std::nothrow) amh_handle();
   if (!h) return fail(nullptr, AMH_ENOMEM, "amh_create: out of memory");
@@ -145,6 +145,8 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
   if (dm != h->cfg.dim)
     return fail(h, AMH_EINVAL, "amh_bind_model: model dimension " + std::to_string(dm) + " != config dim " +
                                    std::to_string(h->cfg.dim));
+  if (dm > 64 && !amh::big_model(model_id, dm))
+    return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model with d a multiple of 32 (<= 256)");
   h->model_id = model_id;
   h->model.data = data;
   h->model.n = (model_id == AMH_MODEL_KIDIQ || model_id == AMH_MODEL_DIAMONDS) ? iparams[0] : 0;
@@ -170,7 +172,13 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
   p.key1 = key[1];
   p.init_z = init_z;
   p.model = h->model;
-  if (amh::split_model(h->model_id, p.d)) {
+  if (amh::big_model(h->model_id, p.d)) {
+    e = amh::run_big_init(p, (hipStream_t)stream);
+    if (e == hipSuccess) {
+      amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model};
+      e = amh::run_big_potential(q, (hipStream_t)stream);
+    }
+  } else if (amh::split_model(h->model_id, p.d)) {
     // pe0 = U(z0) from the lane-per-chain potential (bit-identical to the group one)
     e = amh::run_init_nopot(p, (hipStream_t)stream);
     if (e == hipSuccess) {
@@ -211,6 +219,44 @@ int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_s
   p.gamma_tab = h->gamma_tab;
   p.gamma_tab_n = amh::kGammaTab;
   p.model = h->model;
+  if (amh::big_model(h->model_id, p.d)) {
+    // d > 64: propose pass, MFMA potential, step pass per transition
+    const int64_t C = num_chains;
+    const size_t need = (size_t)C * (size_t)(3 * p.d + 1) * sizeof(float);
+    int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_step/hipMalloc");
+    if (rc != AMH_OK) return rc;
+    amh::BigParams q{};
+    q.out = *out;
+    q.C = C;
+    q.d = p.d;
+    q.W = p.W;
+    q.a = p.a;
+    q.target = p.target;
+    q.eps = p.eps;
+    q.gamma_tab = p.gamma_tab;
+    q.gamma_tab_n = p.gamma_tab_n;
+    q.xprop = h->split_buf;
+    q.wa = q.xprop + (size_t)C * p.d;
+    q.wr = q.wa + (size_t)C * p.d;
+    float* pep = q.wr + (size_t)C * p.d;
+    q.pep = pep;
+    q.accept_count = p.accept_count;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      q.in = (t == 0) ? *in : *out;
+      const bool keep = ((t + 1) % p.thinning) == 0;
+      const int64_t k = t / p.thinning;
+      q.col_z = (keep && p.col_z) ? p.col_z + (size_t)k * C * p.d : nullptr;
+      q.col_pe = (keep && p.col_pe) ? p.col_pe + (size_t)k * C : nullptr;
+      e = amh::run_big_propose(q, (hipStream_t)stream);
+      if (e == hipSuccess) {
+        amh::PotParams pp{q.xprop, pep, C, p.d, h->model};
+        e = amh::run_big_potential(pp, (hipStream_t)stream);
+      }
+      if (e == hipSuccess) e = amh::run_big_step(q, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_step(d > 64)");
+    }
+    return AMH_OK;
+  }
   if (amh::split_model(h->model_id, p.d)) {
     // one transition = propose, batched potential, step(U(z') from memory);
     // collection is per launch: step t keeps slot t / thinning when (t+1) % thinning == 0
@@ -252,8 +298,9 @@ int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* str
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential/hipSetDevice");
   amh::PotParams p{z, pe, n, h->cfg.dim, h->model};
-  e = amh::split_model(h->model_id, p.d) ? amh::run_potential_lane(h->model_id, p, (hipStream_t)stream)
-                                         : amh::run_potential(h->model_id, p, (hipStream_t)stream);
+  e = amh::big_model(h->model_id, p.d)     ? amh::run_big_potential(p, (hipStream_t)stream)
+      : amh::split_model(h->model_id, p.d) ? amh::run_potential_lane(h->model_id, p, (hipStream_t)stream)
+                                           : amh::run_potential(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential");
   return AMH_OK;
 }
@@ -266,6 +313,7 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_sample_pnx: no model bound");
   if (!key || !x || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
     return fail(h, AMH_EINVAL, "amh_sample_pnx: bad arguments");
+  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 not supported");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
   amh::PnxParams p{};
@@ -311,6 +359,7 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
   if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1)
     return fail(h, AMH_EINVAL, "amh_pooled_stats: bad arguments");
+  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_pooled_stats: d > 64 not supported yet");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
   const int d = h->cfg.dim;

@@ -99,6 +99,26 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
 hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);
+// large dimensions (64 < d <= 256, Gaussian; amh_big.hip)
+struct BigParams {
+  amh_state in, out;
+  int64_t C;
+  int32_t d, W;
+  float a, target, eps;
+  const float* gamma_tab;
+  int32_t gamma_tab_n;
+  float *xprop, *wa, *wr;  // propose -> step scratch [C][d]
+  const float* pep;        // U(z') [C]
+  int32_t* accept_count;   // [C] or null
+  float* col_z;            // this step's collection slot [C][d] or null
+  float* col_pe;           // [C] or null
+};
+bool big_model(int model_id, int d);
+hipError_t run_big_init(const InitParams& p, hipStream_t s);
+hipError_t run_big_propose(const BigParams& p, hipStream_t s);
+hipError_t run_big_step(const BigParams& p, hipStream_t s);
+hipError_t run_big_potential(const PotParams& p, hipStream_t s);
+
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain
 // batched potential, then the step kernel reading U(z') (amh_split.hip)
 bool split_model(int model_id, int d);

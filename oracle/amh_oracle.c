@@ -224,8 +224,11 @@ static float pot_diamonds(const orc_cfg* cfg, const float* x, int G) {
   return -(((ll + lpb) + lpi) + lps);
 }
 
+static float pot_gaussian_big(const orc_cfg* cfg, const float* x);
+
 float orc_potential1(const orc_cfg* cfg, const float* x) {
   const int G = orc_gw(cfg);
+  if (cfg->d > ORC_DMAX) return (cfg->model_id == ORC_GAUSSIAN) ? pot_gaussian_big(cfg, x) : NAN;
   switch (cfg->model_id) {
     case ORC_GAUSSIAN: return pot_gaussian(cfg, x, G);
     case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
@@ -463,10 +466,18 @@ static void chain_store(const orc_cfg* cfg, const chain_t* s, int64_t c, const f
 /* n_steps transitions of chains [0, C), in place (one kernel launch).  If
  * collect_z is given it receives z after every step: collect_z[t][c][r].
  * accept_count (nullable) is incremented per accepted proposal. */
+static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe,
+                         float* macc, float* mu, float* L, float* lam, float* asc, const uint32_t* keys,
+                         int32_t* accept_count, float* collect_z);
+
 void orc_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe,
               float* macc, float* mu, float* L, float* lam, float* asc, const uint32_t* keys,
               int32_t* accept_count, float* collect_z) {
   const int d = cfg->d;
+  if (d > ORC_DMAX) {
+    orc_step_big(cfg, C, n_steps, i_, z, pe, macc, mu, L, lam, asc, keys, accept_count, collect_z);
+    return;
+  }
 #pragma omp parallel for schedule(dynamic, 16)
   for (int64_t c = 0; c < C; ++c) {
     chain_t* s = (chain_t*)malloc(sizeof(chain_t));
@@ -765,4 +776,227 @@ int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float
   *macc = maccn;
   *lam = lamn;
   return ok;
+}
+
+/* ====================================== large dimensions (64 < d <= 256) ==== */
+/* Dense Gaussian only, d a multiple of 32 (amh_big.hip).  Kernel mirror:
+ *
+ * potential  batched over chains on MFMA (v_mfma_f32_32x32x2_f32, a k-ordered
+ *            fmaf chain): y_r = fmaf chain over k = 0..d-1 of P_rk D_k with
+ *            D = x - m; q_r = D_r y_r; each 32-row tile I is summed as two
+ *            sequential halves over the accumulator layout (rows (reg & 3) +
+ *            8 (reg >> 2) + 4 h, reg = 0..15, h = 0, 1), t_I = p_I0 + p_I1,
+ *            S = sequential sum of t_I over I; U = 0.5 S + c0.
+ * transition one wave per chain, lane l holds rows r = 64 s + l (slots s).
+ *            propose pass (column order j = 0..d-1): acc_r = fmaf chain of
+ *            U_rj eta_j over j <= r (U_rr = 1); at column r the row's
+ *            proposal is complete and both forward solves of the rank-one
+ *            update finalise  wa_r = (z'_r - mu_r) - sa_r,
+ *            wr_r = (z_r - mu_r) - sr_r,  with sa_r, sr_r the fmaf chains of
+ *            U_rj wa_j, U_rj wr_j over j < r (w = U^-1 delta for the accepted
+ *            and the rejected delta).  Step pass: b by a 64-lane scan per slot
+ *            plus carries, then column order again: s_r = fmaf(U_rj, ws_j,
+ *            s_r), w = delta_r - s_r, U'_rj = fmaf(c_j, w, U_rj) for r > j
+ *            (U'_jj stays 1), as_change terms sequential per row; row sums
+ *            by the 64-lane butterfly per slot, then (s0 + s1) + (s2 + s3).
+ *            Each step is one launch sequence (state through HBM). */
+#define ORC_BIG 256
+
+static float pot_gaussian_big(const orc_cfg* cfg, const float* x) {
+  const int d = cfg->d;
+  const float* m = cfg->data;
+  const float* P = cfg->data + d;
+  const float c0 = cfg->data[d + d * d];
+  float D[ORC_BIG], q[ORC_BIG];
+  for (int k = 0; k < d; ++k) D[k] = x[k] - m[k];
+  for (int r = 0; r < d; ++r) {
+    float y = 0.0f;
+    for (int k = 0; k < d; ++k) y = fmaf(P[r * d + k], D[k], y);
+    q[r] = D[r] * y;
+  }
+  float S = 0.0f;
+  for (int I = 0; I < d / 32; ++I) {
+    float ph[2];
+    for (int h = 0; h < 2; ++h) {
+      float p = 0.0f;
+      for (int reg = 0; reg < 16; ++reg) p = p + q[32 * I + (reg & 3) + 8 * (reg >> 2) + 4 * h];
+      ph[h] = p;
+    }
+    S = S + (ph[0] + ph[1]);
+  }
+  return (0.5f * S) + c0;
+}
+
+/* sum over rows: 64-lane butterfly per slot, then (s0 + s1) + (s2 + s3) */
+static float big_sum(const float* v, int d) {
+  float sl[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  for (int k = 0; k < 4; ++k) {
+    float x[64];
+    for (int l = 0; l < 64; ++l) x[l] = (64 * k + l < d) ? v[64 * k + l] : 0.0f;
+    sl[k] = group_sum(x, 64);
+  }
+  return (sl[0] + sl[1]) + (sl[2] + sl[3]);
+}
+
+/* exclusive scan over rows: 64-lane scan per slot plus the carry of the
+ * slots before (carry_s = carry_{s-1} + total_{s-1}) */
+static void big_excl_scan(const float* t, float* out, int d) {
+  float carry = 0.0f;
+  for (int k = 0; k < 4; ++k) {
+    float x[64], e[64];
+    for (int l = 0; l < 64; ++l) x[l] = (64 * k + l < d) ? t[64 * k + l] : 0.0f;
+    group_excl_scan(x, e, 64);
+    for (int l = 0; l < 64; ++l)
+      if (64 * k + l < d) out[64 * k + l] = (k == 0) ? e[l] : e[l] + carry;
+    const float tot = e[63] + x[63];
+    carry = (k == 0) ? tot : carry + tot;
+  }
+}
+
+typedef struct {
+  float z[ORC_BIG], mu[ORC_BIG], dl[ORC_BIG], inv[ORC_BIG];
+  float U[ORC_BIG][ORC_BIG]; /* U_rj = L_rj / L_jj for r > j (others unused) */
+} bigchain_t;
+
+/* one transition of chain c in place (propose pass, potential, step pass) */
+static int big_step1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t* i_, float* z, float* pe, float* macc,
+                     float* mu, float* L, float* lam, float* asc, const uint32_t* keys) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  float* Lc = L + c * P;
+  for (int r = 0; r < d; ++r) {
+    s->dl[r] = Lc[col_off(d, r)];
+    s->inv[r] = (amh_isfinite(s->dl[r]) && s->dl[r] != 0.0f) ? 1.0f / s->dl[r] : 0.0f;
+    s->z[r] = z[c * d + r];
+    s->mu[r] = mu[c * d + r];
+  }
+  for (int j = 0; j < d; ++j)
+    for (int r = j + 1; r < d; ++r) s->U[r][j] = Lc[col_off(d, j) + (r - j)] * s->inv[j];
+  const int32_t it = i_[c];
+  const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
+  float xi[ORC_BIG], eta[ORC_BIG], acc[ORC_BIG], sa[ORC_BIG], sr[ORC_BIG], zp[ORC_BIG], wa[ORC_BIG], wr[ORC_BIG];
+  uint32_t ubits = 0;
+  for (int r = 0; r < d; ++r) {
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+    xi[r] = amh_normal_from_bits(o.v[0]);
+    if (r == 0) ubits = o.v[1];
+    eta[r] = s->dl[r] * xi[r];
+    acc[r] = sa[r] = sr[r] = 0.0f;
+  }
+  const float u = amh_unif01_from_bits(ubits);
+  const float el = amh_expf(lam[c]);
+  /* propose pass */
+  for (int j = 0; j < d; ++j) {
+    acc[j] = fmaf(1.0f, eta[j], acc[j]);
+    zp[j] = s->z[j] + fmaf(el, acc[j], cfg->eps * xi[j]);
+    wa[j] = (zp[j] - s->mu[j]) - sa[j];
+    wr[j] = (s->z[j] - s->mu[j]) - sr[j];
+    for (int r = j + 1; r < d; ++r) {
+      const float uo = s->U[r][j];
+      acc[r] = fmaf(uo, eta[j], acc[r]);
+      sa[r] = fmaf(uo, wa[j], sa[r]);
+      sr[r] = fmaf(uo, wr[j], sr[r]);
+    }
+  }
+  float pep = pot_gaussian_big(cfg, zp);
+  if (amh_isnan(pep)) pep = INFINITY;
+  /* step pass */
+  const float ex = amh_expf(pe[c] - pep);
+  const float alpha = (ex > 1.0f) ? 1.0f : ex;
+  const int accept = u < alpha;
+  const int32_t itr = it + 1;
+  const int32_t n = (it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  const float maccn = macc[c] + (alpha - macc[c]) / (float)n;
+  float delta[ORC_BIG], ws[ORC_BIG], t[ORC_BIG], gw2[ORC_BIG], Dg[ORC_BIG], one[ORC_BIG], bsc[ORC_BIG];
+  float cc[ORC_BIG], qq[ORC_BIG], sacc[ORC_BIG];
+  for (int r = 0; r < d; ++r) {
+    const float zn = accept ? zp[r] : s->z[r];
+    delta[r] = zn - s->mu[r];
+    ws[r] = accept ? wa[r] : wr[r];
+  }
+  const float lamn = lam[c] + gamma * (alpha - cfg->target_accept_prob);
+  const float e1 = amh_expf(lamn);
+  const float sq = sqrtf(1.0f - gamma);
+  for (int r = 0; r < d; ++r) {
+    const float ajj = sq * s->dl[r];
+    Dg[r] = ajj * ajj;
+    one[r] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : NAN;
+    gw2[r] = gamma * (ws[r] * ws[r]);
+    t[r] = gw2[r] / Dg[r];
+  }
+  big_excl_scan(t, bsc, d);
+  int revert = 0;
+  for (int r = 0; r < d; ++r) {
+    const float b = 1.0f + bsc[r];
+    const float g = (b * Dg[r]) + gw2[r];
+    const float dn = g / b;
+    cc[r] = (gamma * ws[r]) / g;
+    qq[r] = sqrtf(dn);
+    revert |= amh_isnan(fmaf(cc[r], 0.0f, one[r]) * qq[r]);
+  }
+  for (int r = 0; r < d; ++r) sacc[r] = 0.0f;
+  if (!revert) {
+    float ac[ORC_BIG], bc[ORC_BIG], sv[ORC_BIG];
+    for (int r = 0; r < d; ++r) {
+      ac[r] = (qq[r] * e1) - (s->dl[r] * el);
+      bc[r] = (cc[r] * qq[r]) * e1;
+      sv[r] = 0.0f;
+    }
+    for (int j = 0; j < d; ++j) {
+      {
+        const float tt = fmaf(1.0f, ac[j], bc[j] * 0.0f);
+        sacc[j] = fmaf(tt, tt, sacc[j]);
+        Lc[col_off(d, j)] = 1.0f * qq[j];
+      }
+      for (int r = j + 1; r < d; ++r) {
+        const float uo = s->U[r][j];
+        sv[r] = fmaf(uo, ws[j], sv[r]);
+        const float w = delta[r] - sv[r];
+        const float un = fmaf(cc[j], w, uo);
+        const float tt = fmaf(uo, ac[j], bc[j] * w);
+        sacc[r] = fmaf(tt, tt, sacc[r]);
+        Lc[col_off(d, j) + (r - j)] = un * qq[j];
+      }
+    }
+  } else {
+    float ac[ORC_BIG];
+    for (int r = 0; r < d; ++r) ac[r] = (s->dl[r] * e1) - (s->dl[r] * el);
+    for (int j = 0; j < d; ++j) {
+      const float t0 = 1.0f * ac[j];
+      sacc[j] = fmaf(t0, t0, sacc[j]);
+      for (int r = j + 1; r < d; ++r) {
+        const float tt = s->U[r][j] * ac[j];
+        sacc[r] = fmaf(tt, tt, sacc[r]);
+      }
+    }
+  }
+  asc[c] = sqrtf(big_sum(sacc, d));
+  for (int r = 0; r < d; ++r) {
+    z[c * d + r] = accept ? zp[r] : s->z[r];
+    mu[c * d + r] = s->mu[r] + gamma * delta[r];
+  }
+  i_[c] = itr;
+  pe[c] = accept ? pep : pe[c];
+  macc[c] = maccn;
+  lam[c] = lamn;
+  return accept;
+}
+
+static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe,
+                         float* macc, float* mu, float* L, float* lam, float* asc, const uint32_t* keys,
+                         int32_t* accept_count, float* collect_z) {
+  const int d = cfg->d;
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t c = 0; c < C; ++c) {
+    bigchain_t* s = (bigchain_t*)malloc(sizeof(bigchain_t));
+    int nacc = 0;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      nacc += big_step1(cfg, s, c, i_, z, pe, macc, mu, L, lam, asc, keys);
+      if (collect_z)
+        for (int r = 0; r < d; ++r) collect_z[((int64_t)t * C + c) * d + r] = z[c * d + r];
+    }
+    if (accept_count) accept_count[c] += nacc;
+    free(s);
+  }
 }

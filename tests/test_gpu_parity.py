@@ -33,7 +33,8 @@ def test_init_bitexact(kind, gpu, orc):
 
 
 @pytest.mark.parametrize("kind,d", [("gaussian", 64), ("gaussian", 5), ("gaussian", 16), ("gaussian", 33),
-                                    ("eight_schools", None), ("kidiq", None), ("diamonds", None)])
+                                    ("eight_schools", None), ("kidiq", None), ("diamonds", None),
+                                    ("gaussian", 96), ("gaussian", 256)])
 def test_potential_bitexact(kind, d, gpu, orc):
     k, st, om, ost = _init(kind, 8, gpu, orc, d=d)
     z = np.random.default_rng(1).normal(size=(1000, om.d)).astype(np.float32)
@@ -107,6 +108,27 @@ def test_split_path_generic_k(gpu, orc):
     z = np.random.default_rng(2).normal(size=(300, K + 1)).astype(np.float32)
     pe = k.potential(torch.as_tensor(z, device=gpu)).cpu().numpy()
     np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
+
+
+@pytest.mark.parametrize("d,C,steps", [(128, 77, 12), (256, 33, 6)])
+def test_big_dim_bitexact(d, C, steps, gpu, orc):
+    """64 < d <= 256 (amh_big.hip: propose pass, MFMA potential, step pass):
+    init, single launches (gamma_1 = 1 keep-L at step 1, the warmup reset at
+    step W + 1) and a multi-step launch with thinned collection, bit for bit."""
+    k, st, om, ost = _init("gaussian", C, gpu, orc, d=d, num_warmup=3)
+    assert_state_bitequal(st, ost, f"d={d} init")
+    acc = np.zeros(C, np.int32)
+    for t in range(steps):
+        st = k.sample(st, (), {})
+        orc.step(om, ost, 1, num_warmup=3, accept_count=acc)
+        torch.cuda.synchronize()
+        assert_state_bitequal(st, ost, f"d={d} step {t}")
+    np.testing.assert_array_equal(k.accept_count.cpu().numpy(), acc)
+    st2, cz, cp = k.run(st, 4, thinning=2, collect_z=True, collect_pe=True)
+    ocz = orc.step(om, ost, 4, num_warmup=3, collect_z=True)
+    torch.cuda.synchronize()
+    assert_state_bitequal(st2, ost, f"d={d} run")
+    np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), ocz[1::2].view(np.uint32))
 
 
 def test_sample_pnx_bitexact(gpu, orc):

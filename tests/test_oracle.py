@@ -78,12 +78,16 @@ def test_nan_potential_rejects():
 
 
 # ------------------------------------------------- C oracle vs literal numpy --
-@pytest.mark.parametrize("kind", ["gaussian", "eight_schools", "kidiq", "diamonds"])
+@pytest.mark.parametrize("kind,dim", [("gaussian", 12), ("eight_schools", None), ("kidiq", None),
+                                      ("diamonds", None), ("gaussian", 128), ("gaussian", 256)])
 @pytest.mark.parametrize("pre_steps", [0, 1, 37])
-def test_oracle_step_matches_literal(kind, pre_steps, orc):
+def test_oracle_step_matches_literal(kind, dim, pre_steps, orc):
+    """One teacher-forced transition (identical noise) of the C oracle against
+    the literal float64 restatement; d = 128 / 256 exercise the large-d bit
+    spec (wave-per-chain passes, MFMA-order potential)."""
     from kernels import PRNGKey
-    _, _, om = make_case(kind, 12 if kind == "gaussian" else None)
-    d, C, W = om.d, 48, 20
+    _, _, om = make_case(kind, dim)
+    d, C, W = om.d, (48 if om.d <= 64 else 12), 20
     st = orc.init(om, PRNGKey(3), C)
     if pre_steps:
         orc.step(om, st, pre_steps, num_warmup=W)
