@@ -53,6 +53,68 @@ __device__ __forceinline__ float big_sum(const float (&v)[kNS]) {
   return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// Column stream of one chain's packed factor (column-major, column j at
+// col_off(d, j)): blocks of 8 columns are contiguous in HBM (and 16-B aligned
+// for d % 32 == 0), so each block is one bulk LDS-DMA of dwordx4 pieces into
+// the wave's double buffer while the previous block is consumed.  LDS reads
+// go through asm (lds_ld1) so the compiler's wait-count pass does not drain
+// the in-flight DMA before them (see amh_device.h).
+constexpr int kColBlk = 8;
+
+__device__ __forceinline__ void issue_block(const float* Lc, int d, int64_t P, int b, float* wbuf, int lane) {
+  const int j0 = kColBlk * b;
+  const int j1 = j0 + kColBlk;
+  const int64_t o0 = col_off(d, j0);
+  const int64_t o1 = (j1 < d) ? col_off(d, j1) : P;
+  const uint32_t bytes = (uint32_t)(o1 - o0) * 4u;
+  const Buf rb(uniform_ptr(Lc + o0), bytes);
+  for (uint32_t o = 0; o < bytes; o += 1024u) {
+    if (o + 16u * (uint32_t)lane < bytes)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb.rs, (lds_void_t*)(wbuf + o / 4u), 16, (int)(o + 16u * lane), 0, 0, 0);
+  }
+}
+
+// f(KB, j, v) for every column j in order, v[K] = L_rj for rows r = 64 K + l
+// (only rows j < r < d are meaningful; the diagonal L_jj is v[j / 64] of
+// lane j % 64).  KB = j / 64 is a compile-time slot index.
+template <class F>
+__device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, float* wb0, float* wb1, int lane,
+                                            F&& f) {
+  const int nb = d / kColBlk;
+  issue_block(Lc, d, P, 0, wb0, lane);
+  static_for<kNS>([&](auto KB) {
+    constexpr int kb = KB;
+    if (64 * kb < d) {
+      for (int bb = 0; bb < 64 / kColBlk; ++bb) {
+        const int b = (64 / kColBlk) * kb + bb;
+        if (b >= nb) break;
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): block b has landed
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads of the other buffer done
+        float* cur = (b & 1) ? wb1 : wb0;
+        if (b + 1 < nb) issue_block(Lc, d, P, b + 1, (b & 1) ? wb0 : wb1, lane);
+        const int64_t ob = col_off(d, kColBlk * b);
+        for (int q = 0; q < kColBlk; ++q) {
+          const int j = kColBlk * b + q;
+          // element (r, j) sits at cur[col_off(d, j) - ob + r - j]
+          const uint32_t a0 = lds_addr(cur) + 4u * (uint32_t)(col_off(d, j) - ob - j + lane);
+          float v[kNS];
+          static_for<kNS>([&](auto K) {
+            if constexpr (K >= kb) {
+              v[K] = lds_ld1<0>(a0 + 256u * K);
+            } else {
+              v[K] = 0.0f;
+            }
+          });
+          lds_wait(v[0], v[1], v[2], v[3]);
+          f(KB, j, v);
+        }
+      }
+    }
+  });
+}
+
 }  // namespace
 
 // --------------------------------------------------------------- init ----
@@ -102,8 +164,12 @@ __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
 
 // ------------------------------------------------------------- propose ----
 __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
+  extern __shared__ float lds_big[];
   const int d = p.d;
   const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb0 = lds_big + (size_t)wv * 2 * kColBlk * d;
+  float* wb1 = wb0 + kColBlk * d;
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
@@ -124,35 +190,31 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
       mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
       acc[K] = sa[K] = sr[K] = zp[K] = wa[K] = wr[K] = 0.0f;
     });
-    static_for<kNS>([&](auto KB) {
+    for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
       constexpr int kb = KB;
-      for (int jl = 0; jl < 64; ++jl) {
-        const int j = 64 * kb + jl;
-        if (j >= d) break;
-        const float etaj = rdl(eta[kb], jl);
-        const float invj = rdl(inv[kb], jl);
-        // row j completes its proposal and both solves at its own column
-        if (lane == jl) {
-          acc[kb] = fmaf(1.0f, etaj, acc[kb]);
-          zp[kb] = zz[kb] + fmaf(el, acc[kb], p.eps * xi[kb]);
-          wa[kb] = (zp[kb] - mu[kb]) - sa[kb];
-          wr[kb] = (zz[kb] - mu[kb]) - sr[kb];
-        }
-        const float waj = rdl(wa[kb], jl);
-        const float wrj = rdl(wr[kb], jl);
-        const float* col = Lc + col_off(d, j) - j;  // col[r] = L_rj
-        static_for<kNS>([&](auto K) {
-          if constexpr (K >= kb) {
-            const int r = 64 * K + lane;
-            if (r > j && r < d) {
-              const float uo = col[r] * invj;
-              acc[K] = fmaf(uo, etaj, acc[K]);
-              sa[K] = fmaf(uo, waj, sa[K]);
-              sr[K] = fmaf(uo, wrj, sr[K]);
-            }
-          }
-        });
+      const int jl = j - 64 * kb;
+      const float etaj = rdl(eta[kb], jl);
+      const float invj = rdl(inv[kb], jl);
+      // row j completes its proposal and both solves at its own column
+      if (lane == jl) {
+        acc[kb] = fmaf(1.0f, etaj, acc[kb]);
+        zp[kb] = zz[kb] + fmaf(el, acc[kb], p.eps * xi[kb]);
+        wa[kb] = (zp[kb] - mu[kb]) - sa[kb];
+        wr[kb] = (zz[kb] - mu[kb]) - sr[kb];
       }
+      const float waj = rdl(wa[kb], jl);
+      const float wrj = rdl(wr[kb], jl);
+      static_for<kNS>([&](auto K) {
+        if constexpr (K >= kb) {
+          const int r = 64 * K + lane;
+          if (r > j && r < d) {
+            const float uo = v[K] * invj;
+            acc[K] = fmaf(uo, etaj, acc[K]);
+            sa[K] = fmaf(uo, waj, sa[K]);
+            sr[K] = fmaf(uo, wrj, sr[K]);
+          }
+        }
+      });
     });
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
@@ -167,8 +229,12 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
 
 // ---------------------------------------------------------------- step ----
 __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
+  extern __shared__ float lds_big[];
   const int d = p.d;
   const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb0 = lds_big + (size_t)wv * 2 * kColBlk * d;
+  float* wb1 = wb0 + kColBlk * d;
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const int64_t nw = (int64_t)gridDim.x * 4;
   for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
@@ -242,65 +308,57 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
         bc[K] = (cc[K] * qq[K]) * e1;
         sv[K] = 0.0f;
       });
-      static_for<kNS>([&](auto KB) {
+      for_columns(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
         constexpr int kb = KB;
-        for (int jl = 0; jl < 64; ++jl) {
-          const int j = 64 * kb + jl;
-          if (j >= d) break;
-          const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
-          const float bcj = rdl(bc[kb], jl), invj = rdl(inv[kb], jl), qj = rdl(qq[kb], jl);
-          const float* col = Lin + col_off(d, j) - j;
-          float* ocol = Lout + col_off(d, j) - j;
-          if (lane == jl) {
-            const float tt = fmaf(1.0f, acj, bcj * 0.0f);
-            sacc[kb] = fmaf(tt, tt, sacc[kb]);
-            ocol[j] = 1.0f * qj;
-          }
-          static_for<kNS>([&](auto K) {
-            if constexpr (K >= kb) {
-              const int r = 64 * K + lane;
-              if (r > j && r < d) {
-                const float uo = col[r] * invj;
-                sv[K] = fmaf(uo, wsj, sv[K]);
-                const float w = delta[K] - sv[K];
-                const float un = fmaf(cj, w, uo);
-                const float tt = fmaf(uo, acj, bcj * w);
-                sacc[K] = fmaf(tt, tt, sacc[K]);
-                ocol[r] = un * qj;
-              }
-            }
-          });
+        const int jl = j - 64 * kb;
+        const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
+        const float bcj = rdl(bc[kb], jl), invj = rdl(inv[kb], jl), qj = rdl(qq[kb], jl);
+        float* ocol = Lout + col_off(d, j) - j;
+        if (lane == jl) {
+          const float tt = fmaf(1.0f, acj, bcj * 0.0f);
+          sacc[kb] = fmaf(tt, tt, sacc[kb]);
+          ocol[j] = 1.0f * qj;
         }
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r > j && r < d) {
+              const float uo = v[K] * invj;
+              sv[K] = fmaf(uo, wsj, sv[K]);
+              const float w = delta[K] - sv[K];
+              const float un = fmaf(cj, w, uo);
+              const float tt = fmaf(uo, acj, bcj * w);
+              sacc[K] = fmaf(tt, tt, sacc[K]);
+              ocol[r] = un * qj;
+            }
+          }
+        });
       });
     } else {
       // factor kept (arwmh.py:191): copied verbatim; as_change = ||L (e1 - e0)||_F
       float ac[kNS];
       static_for<kNS>([&](auto K) { ac[K] = (dl[K] * e1) - (dl[K] * el); });
-      static_for<kNS>([&](auto KB) {
+      for_columns(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
         constexpr int kb = KB;
-        for (int jl = 0; jl < 64; ++jl) {
-          const int j = 64 * kb + jl;
-          if (j >= d) break;
-          const float acj = rdl(ac[kb], jl), invj = rdl(inv[kb], jl);
-          const float* col = Lin + col_off(d, j) - j;
-          float* ocol = Lout + col_off(d, j) - j;
-          if (lane == jl) {
-            const float t0 = 1.0f * acj;
-            sacc[kb] = fmaf(t0, t0, sacc[kb]);
-            ocol[j] = dl[kb];
-          }
-          static_for<kNS>([&](auto K) {
-            if constexpr (K >= kb) {
-              const int r = 64 * K + lane;
-              if (r > j && r < d) {
-                const float x = col[r];
-                const float tt = (x * invj) * acj;
-                sacc[K] = fmaf(tt, tt, sacc[K]);
-                ocol[r] = x;
-              }
-            }
-          });
+        const int jl = j - 64 * kb;
+        const float acj = rdl(ac[kb], jl), invj = rdl(inv[kb], jl);
+        float* ocol = Lout + col_off(d, j) - j;
+        if (lane == jl) {
+          const float t0 = 1.0f * acj;
+          sacc[kb] = fmaf(t0, t0, sacc[kb]);
+          ocol[j] = dl[kb];
         }
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r > j && r < d) {
+              const float x = v[K];
+              const float tt = (x * invj) * acj;
+              sacc[K] = fmaf(tt, tt, sacc[K]);
+              ocol[r] = x;
+            }
+          }
+        });
       });
     }
     const float asc = sqrtf(big_sum(sacc));
@@ -415,12 +473,13 @@ hipError_t run_big_init(const InitParams& p, hipStream_t s) {
   hipLaunchKernelGGL(big_init_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
+static size_t stream_lds(int d) { return (size_t)4 * 2 * kColBlk * d * sizeof(float); }
 hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_propose_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(big_propose_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_step(const BigParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_step_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  hipLaunchKernelGGL(big_step_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_potential(const PotParams& p, hipStream_t s) {
