@@ -348,7 +348,7 @@ static bool pooled_ok(const amh_pooled_state* s) {
 }
 
 int amh_pooled_sums_size(int32_t dim, int64_t* v) {
-  if (dim < 1 || dim > 64 || !v) return fail(nullptr, AMH_EINVAL, "amh_pooled_sums_size: bad arguments");
+  if (dim < 1 || dim > 256 || !v) return fail(nullptr, AMH_EINVAL, "amh_pooled_sums_size: bad arguments");
   *v = (int64_t)dim + (int64_t)dim * (dim + 1) / 2 + 2;
   return AMH_OK;
 }
@@ -359,13 +359,13 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
   if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1)
     return fail(h, AMH_EINVAL, "amh_pooled_stats: bad arguments");
-  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_pooled_stats: d > 64 not supported yet");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
   const int d = h->cfg.dim;
+  const bool big = amh::big_model(h->model_id, d);
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
-  const int64_t n_chunks = (num_chains + chunk - 1) / chunk;
+  const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains) : (num_chains + chunk - 1) / chunk;
   const size_t need = (size_t)n_chunks * (size_t)(d + (int64_t)d * (d + 1) / 2 + 2) * sizeof(double);
   if (need > h->partials_bytes) {
     if (h->partials) {
@@ -393,6 +393,15 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
   p.pe_out = pe_out;
   p.partials = h->partials;
   p.model = h->model;
+  if (big) {
+    const size_t nb = (size_t)num_chains * (size_t)(d + 1) * sizeof(float);
+    int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
+    if (rc != AMH_OK) return rc;
+    e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
+                                  (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(d > 64)");
+    return AMH_OK;
+  }
   e = amh::run_pooled_stats(h->model_id, p, sums, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats");
   return AMH_OK;
@@ -412,7 +421,7 @@ int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state*
   p.sums = sums;
   p.in = *in;
   p.out = *out;
-  e = amh::run_pooled_update(p, (hipStream_t)stream);
+  e = (p.d > 64) ? amh::run_pooled_big_update(p, (hipStream_t)stream) : amh::run_pooled_update(p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update");
   return AMH_OK;
 }

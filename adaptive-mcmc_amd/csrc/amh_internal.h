@@ -93,6 +93,10 @@ struct PooledUpdateParams {
 };
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);
+// large dimensions (amh_big_pooled.hip): chunks of 256 chains
+int64_t pooled_big_chunks(int64_t C);
+hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
+hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);
 hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s);
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);

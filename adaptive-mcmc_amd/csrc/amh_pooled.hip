@@ -223,6 +223,12 @@ __global__ __launch_bounds__(1024) void pooled_reduce_kernel(const double* parti
   if (q == 0 && v < V) sums[v] = tot;
 }
 
+hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, hipStream_t s) {
+  hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, partials, n_chunks, V,
+                     sums);
+  return hipGetLastError();
+}
+
 namespace {
 __device__ __forceinline__ double readlane_f64(double v, int lane) {
   const long long b = __double_as_longlong(v);

@@ -619,10 +619,20 @@ static float orc_potential_g(const orc_cfg* cfg, const float* x, int G) {
 
 /* Per-chain transition with the shared state; writes z/pe out and the
  * pooled sums.  i: shared iteration (noise stream position). */
+static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
+                                 const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
+                                 float* z_out, float* pe_out, double* sums);
+static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
+                                 float* Lpacked, float* lam, float* asc, double* cov);
+
 void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
                       const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
                       float* z_out, float* pe_out, double* sums) {
   const int d = cfg->d;
+  if (d > ORC_DMAX) {
+    orc_pooled_stats_big(cfg, C, i, z, pe, keys, mu, Lpacked, lam, z_out, pe_out, sums);
+    return;
+  }
   const int64_t P = packed_size(d);
   const int64_t V = d + P + 2;
   const int cpw = orc_pooled_cpw(C);
@@ -717,6 +727,7 @@ void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, 
 int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
                       float* Lpacked, float* lam, float* asc, double* cov) {
   const int d = cfg->d;
+  if (d > ORC_DMAX) return orc_pooled_update_big(cfg, sums, i_, macc, mu, Lpacked, lam, asc, cov);
   const int64_t P = packed_size(d);
   const double N = sums[d + P + 1];
   const int32_t it = *i_;
@@ -999,4 +1010,154 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
     if (accept_count) accept_count[c] += nacc;
     free(s);
   }
+}
+
+/* ------------------------------------- pooled mode, large dimensions ---- */
+/* Kernel mirror (amh_big_pooled.hip):
+ *  proposal  z' = z + fmaf(e^lam, acc, eps xi), acc_r = fmaf chain over
+ *            k < 32 (floor(r / 32) + 1) of L_rk xi_k (L_rk = 0 above the
+ *            diagonal; MFMA on 32-row tiles), U(z') in the MFMA order.
+ *  sums      chunks of 256 consecutive chains: float32 S_dd (fmaf chain over
+ *            the chunk's chains in order, MFMA), S_d and S_a (sequential
+ *            adds), written in double; chunks reduced as in the d <= 64 mode.
+ *  update    Sigma' in double as the d <= 64 mode; its Cholesky factor in
+ *            float32 (element (r, k) updated in column order j < k, then
+ *            divided by L_kk = sqrtf(A_kk)); as_change per row sequential,
+ *            rows by big_sum. */
+#define ORC_BIG_CHUNK 256
+
+static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
+                                 const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
+                                 float* z_out, float* pe_out, double* sums) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const int64_t V = d + P + 2;
+  const int64_t n_chunks = (C + ORC_BIG_CHUNK - 1) / ORC_BIG_CHUNK;
+  const float el = amh_expf(lam);
+  double* part = (double*)calloc((size_t)(n_chunks * V), sizeof(double));
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t ch = 0; ch < n_chunks; ++ch) {
+    float* S = (float*)calloc((size_t)d * d, sizeof(float));
+    float sd[ORC_BIG], xi[ORC_BIG], zp[ORC_BIG], dl[ORC_BIG];
+    float sa = 0.0f;
+    double cnt = 0.0;
+    for (int r = 0; r < d; ++r) sd[r] = 0.0f;
+    for (int64_t c = ch * ORC_BIG_CHUNK; c < C && c < (ch + 1) * ORC_BIG_CHUNK; ++c) {
+      cnt += 1.0;
+      const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
+      uint32_t ubits = 0;
+      for (int r = 0; r < d; ++r) {
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)i, 0u, AMH_TAG_STEP, k0, k1);
+        xi[r] = amh_normal_from_bits(o.v[0]);
+        if (r == 0) ubits = o.v[1];
+      }
+      const float u = amh_unif01_from_bits(ubits);
+      for (int r = 0; r < d; ++r) {
+        float acc = 0.0f;
+        const int kend = 32 * (r / 32 + 1);
+        for (int k = 0; k < kend; ++k) {
+          const float lrk = (k <= r) ? Lpacked[col_off(d, k) + (r - k)] : 0.0f;
+          acc = fmaf(lrk, xi[k], acc);
+        }
+        zp[r] = z[c * d + r] + fmaf(el, acc, cfg->eps * xi[r]);
+      }
+      float pep = pot_gaussian_big(cfg, zp);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe[c] - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      const int accept = u < alpha;
+      for (int r = 0; r < d; ++r) {
+        const float zn = accept ? zp[r] : z[c * d + r];
+        z_out[c * d + r] = zn;
+        dl[r] = zn - mu[r];
+      }
+      pe_out[c] = accept ? pep : pe[c];
+      for (int r = 0; r < d; ++r) {
+        sd[r] = sd[r] + dl[r];
+        for (int k = 0; k <= r; ++k) S[r * d + k] = fmaf(dl[r], dl[k], S[r * d + k]);
+      }
+      sa = sa + alpha;
+    }
+    double* acc = part + ch * V;
+    for (int r = 0; r < d; ++r) acc[r] = (double)sd[r];
+    for (int k = 0; k < d; ++k)
+      for (int r = k; r < d; ++r) acc[d + col_off(d, k) + (r - k)] = (double)S[r * d + k];
+    acc[d + P] = (double)sa;
+    acc[d + P + 1] = cnt;
+    free(S);
+  }
+  const int64_t n_groups = (n_chunks + 15) / 16;
+  for (int64_t v = 0; v < V; ++v) {
+    double tot = 0.0;
+    for (int64_t g = 0; g < n_groups; ++g) {
+      double s = 0.0;
+      for (int64_t c2 = g * 16; c2 < n_chunks && c2 < (g + 1) * 16; ++c2) s += part[c2 * V + v];
+      tot += s;
+    }
+    sums[v] = tot;
+  }
+  free(part);
+}
+
+static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
+                                 float* Lpacked, float* lam, float* asc, double* cov) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const double N = sums[d + P + 1];
+  const int32_t it = *i_;
+  const int32_t itr = it + 1;
+  const int32_t n = (it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  const float abar = (float)(sums[d + P] / N);
+  const float maccn = *macc + (abar - *macc) / (float)n;
+  const float lamn = *lam + gamma * (abar - cfg->target_accept_prob);
+  for (int r = 0; r < d; ++r) mu[r] = mu[r] + gamma * (float)(sums[r] / N);
+  const double g = (double)gamma;
+  double* Sn = (double*)malloc(sizeof(double) * (size_t)P);
+  float* A = (float*)malloc(sizeof(float) * (size_t)d * d);
+  for (int k = 0; k < d; ++k)
+    for (int r = k; r < d; ++r) {
+      const int64_t o = col_off(d, k) + (r - k);
+      const double a = (1.0 - g) * cov[o];
+      const double b = g * (sums[d + o] / N);
+      Sn[o] = a + b;
+      A[r * d + k] = (float)Sn[o];
+    }
+  int ok = 1;
+  for (int j = 0; j < d && ok; ++j) {
+    const float piv = A[j * d + j];
+    if (!(piv > 0.0f) || !amh_isfinite(piv)) { ok = 0; break; }
+    const float ljj = sqrtf(piv);
+    for (int r = j + 1; r < d; ++r) A[r * d + j] = A[r * d + j] / ljj;
+    A[j * d + j] = ljj;
+    for (int k = j + 1; k < d; ++k)
+      for (int r = k; r < d; ++r) A[r * d + k] = fmaf(-A[r * d + j], A[k * d + j], A[r * d + k]);
+  }
+  const float e0 = amh_expf(*lam), e1 = amh_expf(lamn);
+  float part[ORC_BIG];
+  for (int r = 0; r < d; ++r) {
+    float sacc = 0.0f;
+    for (int j = 0; j <= r; ++j) {
+      const float lo = Lpacked[col_off(d, j) + (r - j)];
+      const float ln = ok ? A[r * d + j] : lo;
+      const float tt = (ln * e1) - (lo * e0);
+      sacc = fmaf(tt, tt, sacc);
+    }
+    part[r] = sacc;
+  }
+  *asc = sqrtf(big_sum(part, d));
+  if (ok) {
+    for (int k = 0; k < d; ++k)
+      for (int r = k; r < d; ++r) {
+        const int64_t o = col_off(d, k) + (r - k);
+        Lpacked[o] = A[r * d + k];
+        cov[o] = Sn[o];
+      }
+  }
+  free(Sn);
+  free(A);
+  *i_ = itr;
+  *macc = maccn;
+  *lam = lamn;
+  return ok;
 }

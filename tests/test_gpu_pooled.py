@@ -43,7 +43,8 @@ def _run(kind, d, C, steps, gpu, orc, seed=0):
 
 @pytest.mark.parametrize("kind,d,C,steps", [("gaussian", 64, 3000, 6), ("gaussian", 64, 70000, 3),
                                             ("gaussian", 7, 517, 8), ("eight_schools", None, 64, 8),
-                                            ("kidiq", None, 100, 5), ("diamonds", None, 40, 3)])
+                                            ("kidiq", None, 100, 5), ("diamonds", None, 40, 3),
+                                            ("gaussian", 128, 700, 4), ("gaussian", 256, 600, 3)])
 def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
     _run(kind, d, C, steps, gpu, orc)
 

@@ -136,3 +136,42 @@ def test_two_ranks_match_one(tmp_path, orc):
     np.testing.assert_allclose(g["mu"], sh["mu"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(g["L"], sh["L"], rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(g["z"], z, rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("d", [128, 256])
+def test_one_chain_big_is_the_reference_recurrence(d, orc):
+    """Large-d pooled spec (float32 refactorisation, MFMA-order proposal and
+    potential) with ONE chain against the literal float64 restatement of
+    ARWMH.sample driven by the same noise, 40 steps (W = 10 covers the
+    gamma_1 = 1 keep-L quirk twice)."""
+    import arwmh_np as lit
+    import posteriors as P
+    from kernels import PRNGKey
+    g = P.correlated_gaussian(d)
+    data, _ = g.pack("cpu")
+    om = orc.Model(orc.GAUSSIAN, d, data.numpy())
+    m, Pm, c0 = (data.numpy().astype(np.float64)[:d], data.numpy().astype(np.float64)[d:d + d * d].reshape(d, d),
+                 float(data[d + d * d]))
+    U = lambda z: lit.gaussian_potential(z, m, Pm, c0)  # noqa: E731
+    keys = orc.chain_keys(PRNGKey(5), 0, 1)
+    z = np.random.default_rng(d).uniform(-2, 2, size=(1, d)).astype(np.float32)
+    pe = orc.potential(om, z)
+    sh = orc.pooled_init_shared(d)
+    sh["mu"][:] = z[0]
+    W = 10
+    ref = lit.ARWMHState(0, z[0].astype(np.float64), float(pe[0]), 0.0,
+                         lit.ARWMHAdaptState(z[0].astype(np.float64), np.eye(d), 0.0), 0.0, None)
+    for t in range(40):
+        bits, ubits = lit.step_noise(keys, int(sh["i"][0]), d)
+        xi, u = lit.normal_from_bits(bits[0]), float(lit.unif01_from_bits(ubits[0]))
+        zo, po, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        ref, acc, alpha = lit.sample(ref, U, xi, u, num_warmup=W)
+        assert (not np.array_equal(zo, z)) == bool(acc), f"step {t + 1}"
+        z, pe = zo, po
+        orc.pooled_update(om, sums, sh, num_warmup=W)
+        np.testing.assert_allclose(z[0], ref.z, rtol=1e-4, atol=1e-4)
+        np.testing.assert_allclose(sh["mu"], ref.adapt_state.loc, rtol=1e-4, atol=1e-4)
+        assert abs(sh["lam"][0] - ref.adapt_state.log_step_size) < 1e-4
+        L1 = _unpack(sh["L"], d)
+        Lr = ref.adapt_state.scale
+        assert np.max(np.abs(L1 @ L1.T - Lr @ Lr.T)) <= 1e-3 * np.max(np.abs(Lr @ Lr.T)) + 1e-5, f"step {t + 1}"
