@@ -421,18 +421,36 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
   const bool has0 = 2 * w < nt;
   const float* prow0 = Pm + (int64_t)(32 * (2 * w) + i) * d;
   const float* prow1 = Pm + (int64_t)(32 * (2 * w + 1) + i) * d;
+  // A operands (P rows, L2) in batches of 8 k-steps, the next batch loaded
+  // while the current one feeds the MFMAs
   if (has0) {
-    for (int kk = 0; kk < d; kk += 2) {
-      const float b0 = Dt[(kk + h) * kPotLd + i];
-      const float b1 = Dt[(kk + h) * kPotLd + 32 + i];
-      const float a0 = prow0[kk + h];
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-      if (has1) {
-        const float a1 = prow1[kk + h];
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-      }
+    constexpr int NB = 8;
+    float an0[NB], an1[NB];
+    auto load = [&](int kk0) {
+      static_for<NB>([&](auto S) {
+        an0[S] = prow0[kk0 + 2 * S + h];
+        an1[S] = has1 ? prow1[kk0 + 2 * S + h] : 0.0f;
+      });
+    };
+    load(0);
+    for (int kk0 = 0; kk0 < d; kk0 += 2 * NB) {
+      float a0[NB], a1[NB];
+      static_for<NB>([&](auto S) {
+        a0[S] = an0[S];
+        a1[S] = an1[S];
+      });
+      if (kk0 + 2 * NB < d) load(kk0 + 2 * NB);
+      static_for<NB>([&](auto S) {
+        const int kk = kk0 + 2 * S;
+        const float b0 = Dt[(kk + h) * kPotLd + i];
+        const float b1 = Dt[(kk + h) * kPotLd + 32 + i];
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[S], b0, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0[S], b1, acc[0][1], 0, 0, 0);
+        if (has1) {
+          acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[S], b0, acc[1][0], 0, 0, 0);
+          acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1[S], b1, acc[1][1], 0, 0, 0);
+        }
+      });
     }
   }
   // q = D_r y_r summed over the accumulator layout, then the two lane halves

@@ -39,8 +39,7 @@ __global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsPara
   extern __shared__ float lds[];
   const int d = p.d;
   const int nt = d / 32;
-  float* Xi = lds;
-  float* Zt = lds + (size_t)d * kLd;
+  float* Xi = lds;  // [k][chain]: the noise, then e^lam L xi + eps xi
   const int32_t it = p.i[0];
   const float el = amh_expf(p.lam[0]);
   const int64_t c0 = (int64_t)blockIdx.x * 64;
@@ -51,30 +50,63 @@ __global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsPara
     const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)it, 0u, AMH_TAG_STEP, p.keys[2 * ch],
                                           p.keys[2 * ch + 1]);
     Xi[k * kLd + cc] = amh_normal_from_bits(o.v[0]);
-    Zt[k * kLd + cc] = p.z[ch * d + k];
   }
   __syncthreads();
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
   const int h = lane >> 5, i = lane & 31;
+  // wave w owns row tiles w and nt-1-w (equal triangular work)
+  f32x16 acc[2][2];
+  static_for<2>([&](auto I2) { static_for<2>([&](auto T) { acc[I2][T] = f32x16{}; }); });
+  constexpr int NB = 8;
   static_for<2>([&](auto I2) {
-    const int tile = 2 * w + I2;
-    if (tile < nt) {
+    const int tile = I2 == 0 ? w : nt - 1 - w;
+    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
+    if (own) {
       const int row = 32 * tile + i;
-      f32x16 acc0 = f32x16{}, acc1 = f32x16{};
-      for (int kk = 0; kk < 32 * (tile + 1); kk += 2) {
-        const int col = kk + h;
-        const float a = (row >= col) ? p.L[pk(d, row, col)] : 0.0f;
-        acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Xi[col * kLd + i], acc0, 0, 0, 0);
-        acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Xi[col * kLd + 32 + i], acc1, 0, 0, 0);
+      const int kend = 32 * (tile + 1);
+      float an[NB];
+      auto load = [&](int kk0) {
+        static_for<NB>([&](auto S) {
+          const int col = kk0 + 2 * S + h;
+          an[S] = (row >= col) ? p.L[pk(d, row, col)] : 0.0f;
+        });
+      };
+      load(0);
+      for (int kk0 = 0; kk0 < kend; kk0 += 2 * NB) {
+        float a[NB];
+        static_for<NB>([&](auto S) { a[S] = an[S]; });
+        if (kk0 + 2 * NB < kend) load(kk0 + 2 * NB);
+        static_for<NB>([&](auto S) {
+          const int col = kk0 + 2 * S + h;
+          acc[I2][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[S], Xi[col * kLd + i], acc[I2][0], 0, 0, 0);
+          acc[I2][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[S], Xi[col * kLd + 32 + i], acc[I2][1], 0, 0, 0);
+        });
       }
-      // z' in place of z: each (row, chain) is owned by exactly one lane
+    }
+  });
+  // every wave has read all of Xi: replace it by fmaf(e^lam, L xi, eps xi)
+  float v[2][2][16];
+  static_for<2>([&](auto I2) {
+    const int tile = I2 == 0 ? w : nt - 1 - w;
+    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
+    if (own) {
       static_for<16>([&](auto R) {
         const int rr = 32 * tile + (R & 3) + 8 * (R >> 2) + 4 * h;
-        float* z0 = &Zt[rr * kLd + i];
-        float* z1 = &Zt[rr * kLd + 32 + i];
-        *z0 = *z0 + fmaf(el, acc0[(int)R], p.eps * Xi[rr * kLd + i]);
-        *z1 = *z1 + fmaf(el, acc1[(int)R], p.eps * Xi[rr * kLd + 32 + i]);
+        v[I2][0][R] = fmaf(el, acc[I2][0][(int)R], p.eps * Xi[rr * kLd + i]);
+        v[I2][1][R] = fmaf(el, acc[I2][1][(int)R], p.eps * Xi[rr * kLd + 32 + i]);
+      });
+    }
+  });
+  __syncthreads();
+  static_for<2>([&](auto I2) {
+    const int tile = I2 == 0 ? w : nt - 1 - w;
+    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
+    if (own) {
+      static_for<16>([&](auto R) {
+        const int rr = 32 * tile + (R & 3) + 8 * (R >> 2) + 4 * h;
+        Xi[rr * kLd + i] = v[I2][0][R];
+        Xi[rr * kLd + 32 + i] = v[I2][1][R];
       });
     }
   });
@@ -82,7 +114,7 @@ __global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsPara
   for (int idx = threadIdx.x; idx < 64 * d; idx += 256) {
     const int cc = idx / d, k = idx - cc * d;
     const int64_t ch = c0 + cc;
-    if (ch < p.C) xprop[ch * d + k] = Zt[k * kLd + cc];
+    if (ch < p.C) xprop[ch * d + k] = p.z[ch * d + k] + Xi[k * kLd + cc];
   }
 }
 
@@ -164,7 +196,16 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
     static_for<5>([&](auto S) {
       if (w + 8 * S < npairs) {
         const int ra = (32 * pI[S] + i) * kLd, rb = (32 * pJ[S] + i) * kLd;
-        for (int kk = 0; kk < nv; kk += 2) {
+        int kk = 0;
+        for (; kk + 16 <= nv; kk += 16) {
+          float a[8], b[8];
+          static_for<8>([&](auto Q) {
+            a[Q] = Dl[ra + kk + 2 * Q + h];
+            b[Q] = Dl[rb + kk + 2 * Q + h];
+          });
+          static_for<8>([&](auto Q) { acc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], acc[S], 0, 0, 0); });
+        }
+        for (; kk < nv; kk += 2) {
           acc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(Dl[ra + kk + h], Dl[rb + kk + h], acc[S], 0, 0, 0);
         }
       }
@@ -189,16 +230,56 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
 }
 
 // ------------------------------------------------------------------ update --
+// Diagnostic build (make stamps, tools/upd_stamps.py): thread 0's s_memtime
+// totals per phase: init, diagonal blocks, panel solves, trailing updates,
+// write-out, as_change rows, final reduction.
+#ifdef AMH_STAMPS
+__device__ unsigned long long g_upd_stamps[8];
+#define US_INIT                                   \
+  unsigned long long us_acc[8] = {0};             \
+  unsigned long long us_prev = __builtin_amdgcn_s_memtime();
+#define US(k)                                                 \
+  {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    us_acc[k] += t_ - us_prev;                                \
+    us_prev = t_;                                             \
+  }
+#define US_FLUSH \
+  if (threadIdx.x == 0) for (int k_ = 0; k_ < 8; ++k_) g_upd_stamps[k_] = us_acc[k_];
+hipError_t diag_upd_stamps_copy(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_upd_stamps), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define US_INIT
+#define US(k)
+#define US_FLUSH
+#endif
+
+// LDS layout of the update ("A4"): column-major lower triangle where column j
+// holds rows (j & ~3) .. d-1 (its first j & 3 slots are padding).  Column
+// starts are multiples of 4 floats, so rows 4q .. 4q+3 of any column are one
+// aligned 16-B vector: d(d+4)/2 floats, 133,120 B at d = 256.
+__device__ __forceinline__ int a4_col(int d, int j) {
+  const int q = j >> 2;
+  return 4 * (q * d - 2 * q * (q - 1)) + (j & 3) * (d - 4 * q);
+}
+// index of row 0 of column j (rows r >= (j & ~3) are valid)
+__device__ __forceinline__ int a4_base(int d, int j) { return a4_col(d, j) - (j & ~3); }
+
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
 __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdateParams p) {
-  extern __shared__ float A[];  // packed lower, column-major, float32
+  extern __shared__ __attribute__((aligned(16))) float A[];  // A4 layout, float32
   const int d = p.d;
-  const int64_t P = (int64_t)d * (d + 1) / 2;
   __shared__ int okv;
   __shared__ float rowpart[256];
+  __shared__ __attribute__((aligned(16))) float Lt[32 * 32];  // diagonal block, by column
   const int tid = threadIdx.x;
+  US_INIT
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
   const double* sums = p.sums;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
   const double N = sums[d + P + 1];
   const int32_t it = p.in.i[0];
   const int32_t itr = it + 1;
@@ -210,106 +291,175 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
   const float maccn = macc + (abar - macc) / (float)n;
   const float lamn = lam + gamma * (abar - p.target);
   const double g = (double)gamma;
-  for (int64_t o = tid; o < P; o += 1024) {
-    const double a = (1.0 - g) * p.in.cov[o];
-    const double b = g * (sums[d + o] / N);
-    A[o] = (float)(a + b);
+  // (0) A = float((1-g) Sigma + g S_dd / N): wave w takes columns w, w + 16,
+  // ...; a column's loads are all issued before its LDS stores
+  for (int j = w; j < d; j += 16) {
+    const int64_t co = col_off(d, j);
+    const int len = d - j, ab = a4_base(d, j);
+    double cv[4], sv[4];
+    static_for<4>([&](auto Q) {
+      const int rr = 64 * Q + lane;
+      cv[Q] = rr < len ? p.in.cov[co + rr] : 0.0;
+      sv[Q] = rr < len ? sums[d + co + rr] : 0.0;
+    });
+    static_for<4>([&](auto Q) {
+      const int rr = 64 * Q + lane;
+      if (rr < len) {
+        const double a = (1.0 - g) * cv[Q];
+        const double b = g * (sv[Q] / N);
+        A[ab + j + rr] = (float)(a + b);
+      }
+    });
   }
   if (tid == 0) okv = 1;
   __syncthreads();
+  US(0)
   for (int p0 = 0; p0 < d; p0 += 32) {
-    // (1) diagonal block: wave 0, lane i < 32 holds row p0 + i
+    // (1) diagonal block: wave 0, lane ii (and ii + 32, a duplicate) holds row
+    // p0 + ii.  Column k of the block's factor goes to Lt (dense, Lt[k][m] =
+    // L_{p0+m, p0+k}) and is read back as 16-B broadcasts.  No lane masks: the
+    // entries above the diagonal (m > ii) are updated too and never used, so
+    // nothing row-dependent stays live across the 32 steps.
     if (w == 0) {
       const int ii = lane & 31;
+      const int r = p0 + ii;
       float a[32];
-      static_for<32>([&](auto K) { a[K] = (K <= ii) ? A[pk(d, p0 + ii, p0 + K)] : 0.0f; });
+      static_for<32>([&](auto K) { a[K] = (K <= ii) ? A[a4_base(d, p0 + K) + r] : 0.0f; });
       bool ok = true;
       static_for<32>([&](auto K) {
         constexpr int k = K;
         const float piv = rdlane(a[k], k);
         ok = ok && (piv > 0.0f) && amh_isfinite(piv);
         const float ljj = sqrtf(piv);
-        if (ii > k) a[k] = a[k] / ljj;
-        if (ii == k) a[k] = ljj;
-        static_for<32>([&](auto M) {
-          constexpr int m = M;
-          if constexpr (m > k) {
-            const float lmk = rdlane(a[k], m);
-            if (ii >= m) a[m] = fmaf(-a[k], lmk, a[m]);
-          }
-        });
+        a[k] = a[k] / ljj;
+        Lt[k * 32 + ii] = a[k];
+        Lt[k * 32 + k] = ljj;  // uniform store, after the lane stores
+        if constexpr (k + 1 < 32) {
+          static_for<(32 - ((k + 1) & ~3)) / 4>([&](auto Q) {
+            constexpr int m0 = ((k + 1) & ~3) + 4 * Q;
+            const f32x4 v = *(const f32x4*)&Lt[k * 32 + m0];
+            static_for<4>([&](auto E) {
+              constexpr int m = m0 + E;
+              if constexpr (m > k) a[m] = fmaf(-a[k], v[(int)E], a[m]);
+            });
+          });
+        }
       });
-      if (lane < 32) static_for<32>([&](auto K) { if (K <= ii) A[pk(d, p0 + ii, p0 + K)] = a[K]; });
       if (lane == 0 && !ok) okv = 0;
+      for (int k = 0; k < 32; ++k) {
+        if (lane < 32 && lane >= k) A[a4_base(d, p0 + k) + p0 + lane] = Lt[k * 32 + lane];
+      }
     }
     __syncthreads();
-    // (2) panel below the block: one thread per row
+    US(1)
+    // (2) panel below the block: one thread per row, L_mk of the block as
+    // 16-B broadcasts from Lt
     const int q0 = p0 + 32;
     if (tid < d - q0) {
       const int r = q0 + tid;
       float a[32];
-      static_for<32>([&](auto K) { a[K] = A[pk(d, r, p0 + K)]; });
+      static_for<32>([&](auto K) { a[K] = A[a4_base(d, p0 + K) + r]; });
       static_for<32>([&](auto K) {
         constexpr int k = K;
-        const float lrk = a[k] / A[pk(d, p0 + k, p0 + k)];
+        const float lrk = a[k] / Lt[k * 32 + k];
         a[k] = lrk;
-        static_for<32>([&](auto M) {
-          constexpr int m = M;
-          if constexpr (m > k) a[m] = fmaf(-lrk, A[pk(d, p0 + m, p0 + k)], a[m]);
+        static_for<(32 - ((k + 1) & ~3)) / 4>([&](auto Q) {
+          constexpr int m0 = ((k + 1) & ~3) + 4 * Q;
+          const f32x4 v = *(const f32x4*)&Lt[k * 32 + m0];
+          static_for<4>([&](auto E) {
+            constexpr int m = m0 + E;
+            if constexpr (m > k) a[m] = fmaf(-lrk, v[(int)E], a[m]);
+          });
         });
+        asm volatile("" ::: "memory");  // keep the next column's reads after this one's FMAs
       });
-      static_for<32>([&](auto K) { A[pk(d, r, p0 + K)] = a[K]; });
+      static_for<32>([&](auto K) { A[a4_base(d, p0 + K) + r] = a[K]; });
     }
     __syncthreads();
-    // (3) trailing update with the panel's 32 columns, 4x4 element tiles
-    const int nb = (d - q0) / 4;
+    US(2)
+    // (3) trailing update with the panel's 32 columns: 8x8 element tiles,
+    // packed FMAs (each lane of v_pk_fma_f32 is an fmaf), column j's 8 rows as
+    // two aligned 16-B reads
+    const int nb = (d - q0) / 8;
     for (int tix = tid; tix < nb * (nb + 1) / 2; tix += 1024) {
-      int R = 0;
+      int R = (int)((sqrtf(8.0f * (float)tix + 1.0f) - 1.0f) * 0.5f);
+      while (R * (R + 1) / 2 > tix) --R;
       while ((R + 1) * (R + 2) / 2 <= tix) ++R;
       const int Cb = tix - R * (R + 1) / 2;
-      const int r0 = q0 + 4 * R, c0 = q0 + 4 * Cb;
-      float t[4][4];
-      static_for<4>([&](auto X) {
-        static_for<4>([&](auto Y) {
-          const int r = r0 + X, c = c0 + Y;
-          t[X][Y] = (c <= r) ? A[pk(d, r, c)] : 0.0f;
-        });
+      const int r0 = q0 + 8 * R, c0 = q0 + 8 * Cb;
+      f32x2 t[8][4];
+      static_for<8>([&](auto Y) {
+        const int cbase = a4_base(d, c0 + Y) + r0;
+        static_for<8>([&](auto X) { t[X][(int)Y / 2][(int)Y % 2] = A[cbase + X]; });
       });
       for (int j = 0; j < 32; ++j) {
-        const int64_t cj = col_off(d, p0 + j) - (p0 + j);
-        float lr[4], lc[4];
-        static_for<4>([&](auto X) {
-          lr[X] = A[cj + r0 + X];
-          lc[X] = A[cj + c0 + X];
-        });
-        static_for<4>([&](auto X) {
-          static_for<4>([&](auto Y) { t[X][Y] = fmaf(-lr[X], lc[Y], t[X][Y]); });
+        const int cb = a4_base(d, p0 + j);
+        const f32x4 r4a = *(const f32x4*)&A[cb + r0], r4b = *(const f32x4*)&A[cb + r0 + 4];
+        const f32x4 c4a = *(const f32x4*)&A[cb + c0], c4b = *(const f32x4*)&A[cb + c0 + 4];
+        const float lr[8] = {r4a[0], r4a[1], r4a[2], r4a[3], r4b[0], r4b[1], r4b[2], r4b[3]};
+        const f32x2 lc[4] = {f32x2{c4a[0], c4a[1]}, f32x2{c4a[2], c4a[3]}, f32x2{c4b[0], c4b[1]},
+                             f32x2{c4b[2], c4b[3]}};
+        static_for<8>([&](auto X) {
+          const f32x2 nl = f32x2{-lr[X], -lr[X]};
+          static_for<4>([&](auto Y) { t[X][Y] = __builtin_elementwise_fma(nl, lc[Y], t[X][Y]); });
         });
       }
-      static_for<4>([&](auto X) {
-        static_for<4>([&](auto Y) {
-          const int r = r0 + X, c = c0 + Y;
-          if (c <= r) A[pk(d, r, c)] = t[X][Y];
+      static_for<8>([&](auto Y) {
+        const int c = c0 + Y;
+        const int cbase = a4_base(d, c) + r0;
+        static_for<8>([&](auto X) {
+          if (c <= r0 + X) A[cbase + X] = t[X][(int)Y / 2][(int)Y % 2];
         });
       });
     }
     __syncthreads();
+    US(3)
   }
   const bool ok = okv != 0;
   const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
+  // (4) write-out, column-wise (coalesced); each element's as_change term
+  // replaces it in LDS (in-place safe: the old factor is read before the new
+  // one is written)
+  for (int j = w; j < d; j += 16) {
+    const int64_t co = col_off(d, j);
+    const int len = d - j, ab = a4_base(d, j);
+    float lo[4];
+    double cv[4], sv[4];
+    static_for<4>([&](auto Q) {
+      const int rr = 64 * Q + lane;
+      lo[Q] = rr < len ? p.in.scale[co + rr] : 0.0f;
+      cv[Q] = rr < len ? p.in.cov[co + rr] : 0.0;
+      sv[Q] = (ok && rr < len) ? sums[d + co + rr] : 0.0;
+    });
+    static_for<4>([&](auto Q) {
+      const int rr = 64 * Q + lane;
+      if (rr < len) {
+        const float ln = ok ? A[ab + j + rr] : lo[Q];
+        if (ok) {
+          const double a = (1.0 - g) * cv[Q];
+          const double b = g * (sv[Q] / N);
+          p.out.cov[co + rr] = a + b;
+        } else {
+          p.out.cov[co + rr] = cv[Q];
+        }
+        p.out.scale[co + rr] = ln;
+        A[ab + j + rr] = (ln * e1) - (lo[Q] * e0);
+      }
+    });
+  }
+  __syncthreads();
+  US(4)
   if (tid < d) {
     const int r = tid;
     float s = 0.0f;
     for (int j = 0; j <= r; ++j) {
-      const int64_t o = pk(d, r, j);
-      const float lo = p.in.scale[o];
-      const float ln = ok ? A[o] : lo;
-      const float tt = (ln * e1) - (lo * e0);
+      const float tt = A[a4_base(d, j) + r];
       s = fmaf(tt, tt, s);
     }
     rowpart[r] = s;
   }
   __syncthreads();
+  US(5)
   if (w == 0) {
     float sl[4];
     static_for<4>([&](auto K) { sl[K] = Grp<64>::sum((64 * K + lane < d) ? rowpart[64 * K + lane] : 0.0f); });
@@ -322,17 +472,8 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
     }
   }
   if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
-  for (int64_t o = tid; o < P; o += 1024) {
-    if (ok) {
-      const double a = (1.0 - g) * p.in.cov[o];
-      const double b = g * (sums[d + o] / N);
-      p.out.cov[o] = a + b;
-      p.out.scale[o] = A[o];
-    } else {
-      p.out.cov[o] = p.in.cov[o];
-      p.out.scale[o] = p.in.scale[o];
-    }
-  }
+  US(6)
+  US_FLUSH
 }
 
 // --------------------------------------------------------------- launchers --
@@ -344,7 +485,7 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
   const int d = p.d;
   const int64_t V = d + (int64_t)d * (d + 1) / 2 + 2;
   hipLaunchKernelGGL(pooled_big_propose_kernel, dim3((unsigned)((p.C + 63) / 64)), dim3(256),
-                     (size_t)2 * d * kLd * sizeof(float), s, p, xprop);
+                     (size_t)d * kLd * sizeof(float), s, p, xprop);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   PotParams q{xprop, pep, p.C, d, p.model};
@@ -359,7 +500,7 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
 }
 
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
-  const size_t shm = (size_t)p.d * (p.d + 1) / 2 * sizeof(float);
+  const size_t shm = (size_t)p.d * (p.d + 4) / 2 * sizeof(float);
   hipLaunchKernelGGL(pooled_big_update_kernel, dim3(1), dim3(1024), shm, s, p);
   return hipGetLastError();
 }

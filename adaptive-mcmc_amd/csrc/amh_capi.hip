@@ -445,5 +445,7 @@ int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* i
 int amh_diag_stamps(void* host, int64_t bytes) {
   return amh::diag_stamps_copy(host, (size_t)bytes) == hipSuccess ? 0 : -1;
 }
+// pooled large-d update kernel phase totals (8 x u64)
+int amh_diag_upd_stamps(void* host) { return amh::diag_upd_stamps_copy(host) == hipSuccess ? 0 : -1; }
 #endif
 }  // extern "C"

@@ -52,7 +52,7 @@ def test_calls_fail_cleanly_without_device(lib):
     assert L.amh_create(ctypes.byref(cfg), 0, ctypes.byref(h)) == -3  # AMH_EHIP
     assert L.amh_last_error(None)
     assert L.amh_step(None, 1, None, None, 1, None, None) == -1  # AMH_EINVAL: null handle
-    bad = lib.AmhConfig(65, 0, 2 / 3, 0.234, 1e-6, (ctypes.c_int32 * 3)(0, 0, 0))
+    bad = lib.AmhConfig(257, 0, 2 / 3, 0.234, 1e-6, (ctypes.c_int32 * 3)(0, 0, 0))
     assert L.amh_create(ctypes.byref(bad), 0, ctypes.byref(h)) == -1
     assert b"dim" in L.amh_last_error(None)
 
