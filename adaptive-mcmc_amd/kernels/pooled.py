@@ -62,6 +62,8 @@ class PooledARWMH(ARWMH):
     torch.distributed process group whose chains are pooled (default: the
     default group when initialised, else this process alone)."""
 
+    pooled = True  # adapt-state leaves carry no chain axis
+
     def __init__(self, model=None, potential_fn=None, lr_decay=2 / 3, target_accept_prob=0.234, eps=1e-6,
                  num_chains=None, device=None, chain_offset=0, group=None, **kw):
         super().__init__(model=model, potential_fn=potential_fn, lr_decay=lr_decay,

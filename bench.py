@@ -34,28 +34,11 @@ def bytes_per_chain_step(d: int) -> int:
     return 2 * 4 * (d * (d + 1) // 2 + 2 * d + 6)
 
 
-def ess_geyer(x: np.ndarray) -> float:
-    """Multi-chain ESS of x [chains, draws] (Stan / Geyer initial monotone
-    sequence; the n_eff family of numpyro print_summary)."""
-    m, n = x.shape
-    xc = x - x.mean(axis=1, keepdims=True)
-    f = np.fft.rfft(xc, n=2 * n, axis=1)
-    acov = np.fft.irfft(f * np.conj(f), axis=1)[:, :n] / n
-    var_w = acov[:, 0].mean() * n / (n - 1)
-    var_plus = var_w * (n - 1) / n + (x.mean(axis=1).var(ddof=1) if m > 1 else 0.0)
-    rho = 1.0 - (var_w - acov.mean(axis=0)) / var_plus
-    rho[0] = 1.0
-    t, s, prev = 0, 0.0, np.inf
-    while t + 1 < n:
-        p = rho[t] + rho[t + 1]
-        if p < 0:
-            break
-        p = min(p, prev)
-        s += p
-        prev = p
-        t += 2
-    tau = -1.0 + 2.0 * s
-    return float(m * n / max(tau, 1e-12))
+def ess(x: np.ndarray) -> float:
+    """Multi-chain ESS of x [chains, draws] (numpyro's estimator, the n_eff
+    of print_summary: adaptive-mcmc_amd/infer/diagnostics.py)."""
+    from infer.diagnostics import effective_sample_size
+    return float(effective_sample_size(x))
 
 
 def measured_traffic(C: int, d: int):
@@ -217,8 +200,8 @@ def main():
         el = time.perf_counter() - e0
         zc = cz.cpu().numpy()
         pc = cp.cpu().numpy()
-        vals = [ess_geyer(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
-        vals.append(ess_geyer(pc.T.astype(np.float64)))
+        vals = [ess(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
+        vals.append(ess(pc.T.astype(np.float64)))
         ess = {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T,
                "seconds": el, "coords": [0, 1, d // 2, d - 1, "U"]}
 

@@ -1,0 +1,130 @@
+"""infer.MCMC on the GPU kernels: numpyro MCMC semantics (warmup, thinning
+with remainder, extra fields, constrained samples, summary) and the
+eight-schools posterior the reference prints (posteriordb_eight-schools.ipynb
+cell 28: ARWMH, 5e4 warmup, 5e5 samples, thinning 50)."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _es(gpu, C):
+    import posteriors as P
+    from kernels import ARWMH
+    return ARWMH(model=P.eight_schools, num_chains=C, device=gpu), dict(P.EIGHT_SCHOOLS_DATA)
+
+
+def test_eight_schools_posterior(gpu):
+    """The notebook's run configuration on 256 chains (2.56M kept draws, ~2 s).
+    Shorter runs (5e3 warmup, 5e4 samples) sit visibly high in tau: the
+    funnel's neck is reached late, in the reference's single chain as here."""
+    from infer import MCMC
+    from kernels import PRNGKey
+    C = 256
+    k, data = _es(gpu, C)
+    m = MCMC(k, num_warmup=50000, num_samples=500000, thinning=50)
+    m.run(PRNGKey(0), extra_fields=("potential_energy",), **data)
+    s = m.get_samples()
+    K = 10000
+    assert s["mu"].shape == (C * K,) and s["theta_base"].shape == (C * K, 8)
+    assert s["theta"].shape == (C * K, 8)  # deterministic site (TransformReparam)
+    assert float(s["tau"].min()) > 0
+    pe = m.get_extra_fields()["potential_energy"]
+    assert pe.shape == (C * K,)
+    # notebook: mu 4.40 (sd 3.29), tau 3.63 (3.21), theta_base[0] 0.32 (0.99), min U 40.975
+    assert float(s["mu"].mean()) == pytest.approx(4.40, abs=0.1)
+    assert float(s["mu"].std()) == pytest.approx(3.29, abs=0.1)
+    assert float(s["tau"].mean()) == pytest.approx(3.63, abs=0.1)
+    assert float(s["tau"].std()) == pytest.approx(3.21, abs=0.1)
+    assert float(s["theta_base"][:, 0].mean()) == pytest.approx(0.32, abs=0.03)
+    assert float(s["theta_base"][:, 0].std()) == pytest.approx(0.99, abs=0.04)
+    assert float(pe.min()) == pytest.approx(40.975, abs=0.5)
+    txt = m.summary_str()
+    rows = [ln for ln in txt.split("\n") if ln.strip()]
+    assert len(rows) == 1 + 1 + 1 + 8  # header, mu, tau, theta_base[0..7]; theta excluded
+    assert rows[0] == "                   mean       std    median      5.0%     95.0%     n_eff     r_hat"
+    from infer import diagnostics as D
+    g = m.get_samples(group_by_chain=True)
+    assert g["mu"].shape == (C, K)
+    assert float(D.effective_sample_size(g["mu"])) > 0.5 * C * K
+    assert float(D.split_gelman_rubin(g["tau"])) < 1.01
+    assert float(m.last_state.mean_accept_prob.mean()) == pytest.approx(0.234, abs=0.01)
+
+
+def test_thinning_and_extra_fields_paths(gpu):
+    """z / potential_energy only: one fused launch, the step kernel writes the
+    kept draws.  Any other extra field: one launch per kept draw plus device
+    snapshots.  Each path equals the same launch sequence done by hand, bit for
+    bit; the two differ only at ULP level (a fused launch keeps the factor in
+    unit-lower form between its steps).  Remainder steps come
+    first (numpyro fori_collect)."""
+    from infer import MCMC
+    from kernels import PRNGKey
+    res = []
+    for fields in [("potential_energy",), ("potential_energy", "adapt_state", "mean_accept_prob")]:
+        k, data = _es(gpu, 33)
+        m = MCMC(k, num_warmup=100, num_samples=105, thinning=10)
+        m.run(PRNGKey(3), extra_fields=fields, **data)
+        res.append(m)
+    a, b = res
+    za, zb = a._states["z"], b._states["z"]
+    assert za.shape == (33, 10, 10)
+    assert torch.equal(za[:, -1], a.last_state.z)
+    assert int(a.last_state.i[0]) == 205
+    # by hand: warmup launch, remainder launch, then the two partitions
+    k, data = _es(gpu, 33)
+    st = k.init(PRNGKey(3), 100, None, (), data)
+    k.sample_(st, 100)
+    k.sample_(st, 5)
+    st2 = type(st)(*[x.clone() if hasattr(x, "clone") else type(x)(*[y.clone() for y in x]) for x in st])
+    _, cz, cp = k.run(st, 100, 10, collect_z=True, collect_pe=True)
+    assert torch.equal(za, cz.transpose(0, 1))
+    assert torch.equal(a.get_extra_fields(group_by_chain=True)["potential_energy"], cp.transpose(0, 1))
+    snaps = []
+    for _ in range(10):
+        k.sample_(st2, 10)
+        snaps.append(st2.z.clone())
+    assert torch.equal(zb, torch.stack(snaps, 1))
+    close = torch.isclose(za, zb, rtol=1e-3, atol=1e-4).all(dim=2).all(dim=1)
+    assert float(close.float().mean()) > 0.9
+    ex = b.get_extra_fields(group_by_chain=True)
+    assert ex["adapt_state"].scale.shape == (33, 10, 55)
+    assert ex["mean_accept_prob"].shape == (33, 10)
+    assert torch.equal(ex["adapt_state"].loc[:, -1], b.last_state.adapt_state.loc)
+    with pytest.raises(AttributeError):
+        k, data = _es(gpu, 4)
+        MCMC(k, num_warmup=1, num_samples=2).run(PRNGKey(0), extra_fields=("diverging",), **data)
+
+
+def test_post_warmup_state_continues(gpu):
+    from infer import MCMC
+    from kernels import PRNGKey
+    k, data = _es(gpu, 16)
+    m = MCMC(k, num_warmup=50, num_samples=20)
+    m.warmup(PRNGKey(1), **data)
+    assert int(m.post_warmup_state.i[0]) == 50
+    m.run(PRNGKey(1), **data)
+    assert int(m.last_state.i[0]) == 70
+    k2, _ = _es(gpu, 16)
+    m2 = MCMC(k2, num_warmup=50, num_samples=20)
+    m2.run(PRNGKey(1), **data)
+    assert torch.equal(m.get_samples()["mu"], m2.get_samples()["mu"])
+
+
+def test_pooled_kernel_under_mcmc(gpu):
+    import posteriors as P
+    from infer import MCMC
+    from kernels import PooledARWMH, PRNGKey
+    g = P.correlated_gaussian(16)
+    C = 256
+    k = PooledARWMH(potential_fn=g, num_chains=C, device=gpu)
+    z0 = torch.zeros(C, 16)
+    m = MCMC(k, num_warmup=200, num_samples=40, thinning=4)
+    m.run(PRNGKey(0), init_params=z0, extra_fields=("potential_energy", "adapt_state"))
+    z = m.get_samples(group_by_chain=True)
+    assert z.shape == (C, 10, 16)
+    ex = m.get_extra_fields(group_by_chain=True)
+    assert ex["potential_energy"].shape == (C, 10)
+    assert ex["adapt_state"].loc.shape == (1, 10, 16)
+    assert torch.equal(ex["adapt_state"].scale[0, -1], m.last_state.adapt_state.scale)
