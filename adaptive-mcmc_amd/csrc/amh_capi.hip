@@ -341,6 +341,71 @@ int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint3
   return AMH_OK;
 }
 
+// -------------------------------------------------------------------- ASSS --
+static bool asss_state_ok(const amh_state* s) {
+  return s && s->i && s->z && s->potential_energy && s->loc && s->scale && s->as_change && s->rng_key;
+}
+
+int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out, int32_t n_steps,
+                  const amh_collect* collect, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_asss_step: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_asss_step: no model bound");
+  if (!asss_state_ok(in) || !asss_state_ok(out) || num_chains < 1 || n_steps < 0)
+    return fail(h, AMH_EINVAL, "amh_asss_step: bad arguments");
+  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64");
+  if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_asss_step: thinning must be >= 1");
+  if (n_steps == 0) return AMH_OK;
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_asss_step/hipSetDevice");
+  amh::StepParams p{};
+  p.in = *in;
+  p.out = *out;
+  p.C = num_chains;
+  p.d = h->cfg.dim;
+  p.W = h->cfg.num_warmup;
+  p.a = h->cfg.lr_decay;
+  p.target = h->cfg.target_accept_prob;
+  p.eps = h->cfg.eps;
+  p.n_steps = n_steps;
+  p.thinning = collect ? collect->thinning : 1;
+  p.col_z = collect ? collect->z : nullptr;
+  p.col_pe = collect ? collect->potential_energy : nullptr;
+  p.accept_count = nullptr;
+  p.gamma_tab = h->gamma_tab;
+  p.gamma_tab_n = amh::kGammaTab;
+  p.model = h->model;
+  e = amh::run_asss_step(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_asss_step");
+  return AMH_OK;
+}
+
+int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t n_points, int64_t n_samples,
+                        const float* loc, const float* scale_packed, int32_t n, float* out, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_asss_sample_pnx: null handle");
+  if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_asss_sample_pnx: no model bound");
+  if (!key || !x || !loc || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
+    return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: bad arguments");
+  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx/hipSetDevice");
+  amh::AsssPnxParams p{};
+  p.x = x;
+  p.n_points = n_points;
+  p.n_samples = n_samples;
+  p.loc = loc;
+  p.scale = scale_packed;
+  p.eps = h->cfg.eps;
+  p.n = n;
+  p.d = h->cfg.dim;
+  p.key0 = key[0];
+  p.key1 = key[1];
+  p.out = out;
+  p.model = h->model;
+  e = amh::run_asss_pnx(h->model_id, p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx");
+  return AMH_OK;
+}
+
 // ------------------------------------------------------- pooled covariance --
 static bool pooled_ok(const amh_pooled_state* s) {
   return s && s->i && s->z && s->potential_energy && s->rng_key && s->mean_accept_prob && s->loc && s->scale &&

@@ -146,6 +146,50 @@ struct Grp {
   }
 };
 
+// ----------------------------------------------------------- lane masks --
+// Per-column lane predicates of the load/store phases.  For a full-wave
+// group they are compile-time lane masks built by one SALU shift inside the
+// asm (so the compiler can neither hoist 64 mask constants into SGPRs nor
+// keep them live across the chain loop); smaller groups compare an opaque
+// per-item copy of the lane index.
+template <int G, int J>
+__device__ __forceinline__ float keep_above(float x, int rr) {  // lanes r > J keep x, else 0
+  if constexpr (G == 64) {
+    if constexpr (J >= 63) {
+      return 0.0f;
+    } else {
+      float out;
+      unsigned long long m;
+      asm("s_lshl_b64 %1, -1, %3\n\tv_cndmask_b32_e64 %0, 0, %2, %1" : "=v"(out), "=&s"(m) : "v"(x), "n"(J + 1));
+      return out;
+    }
+  } else {
+    return (rr > J) ? x : 0.0f;
+  }
+}
+template <int G, int J>
+__device__ __forceinline__ float set_one_at(float x, int rr) {  // lane r == J gets 1.0
+  if constexpr (G == 64) {
+    float out;
+    unsigned long long m;
+    asm("s_lshl_b64 %1, 1, %3\n\tv_cndmask_b32_e64 %0, %2, 1.0, %1" : "=v"(out), "=&s"(m) : "v"(x), "n"(J));
+    return out;
+  } else {
+    return (rr == J) ? 1.0f : x;
+  }
+}
+template <int G, int J>
+__device__ __forceinline__ uint32_t off_from(uint32_t v, uint32_t oob, int rr) {  // lanes r >= J keep v, else oob
+  if constexpr (G == 64) {
+    uint32_t out;
+    unsigned long long m;
+    asm("s_lshl_b64 %1, -1, %4\n\tv_cndmask_b32_e64 %0, %3, %2, %1" : "=v"(out), "=&s"(m) : "v"(v), "v"(oob), "n"(J));
+    return out;
+  } else {
+    return (rr >= J) ? v : oob;
+  }
+}
+
 // packed column-major lower triangle: column j starts at j*d - j(j-1)/2
 __device__ __forceinline__ int64_t col_off(int d, int j) {
   return (int64_t)j * d - (int64_t)j * (j - 1) / 2;

@@ -63,6 +63,19 @@ struct PnxParams {
   ModelArgs model;
 };
 
+// ASSS.sample_Pnx (amh_asss.hip): frozen shared (loc, scale) for every chain
+struct AsssPnxParams {
+  const float* x;
+  int64_t n_points, n_samples;
+  const float* loc;    // shared mu [d]
+  const float* scale;  // shared packed factor
+  float eps;
+  int32_t n, d;
+  uint32_t key0, key1;
+  float* out;
+  ModelArgs model;
+};
+
 // pooled covariance (amh_pooled.hip)
 constexpr int kPoolWaves = 16;  // waves (of one chain each) per chunk block
 
@@ -97,6 +110,8 @@ hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* su
 int64_t pooled_big_chunks(int64_t C);
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);
+hipError_t run_asss_step(int model_id, const StepParams& p, hipStream_t s);  // amh_asss.hip
+hipError_t run_asss_pnx(int model_id, const AsssPnxParams& p, hipStream_t s);
 hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s);
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);

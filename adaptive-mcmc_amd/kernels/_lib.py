@@ -24,7 +24,8 @@ AMH_MODEL_DIAMONDS = 4
 # every symbol include/amh.h declares
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",
            "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
-           "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step")
+           "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_asss_step",
+           "amh_asss_sample_pnx")
 
 
 class AmhConfig(ctypes.Structure):
@@ -76,6 +77,11 @@ def lib():
     L.amh_potential.argtypes = [P, P, P, I64, P]
     L.amh_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, F, I32, P, P]
     L.amh_chain_keys.argtypes = [ctypes.POINTER(ctypes.c_uint32), I64, I64, P, P]
+    L.amh_asss_step.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), I32,
+                                ctypes.POINTER(AmhCollect), P]
+    L.amh_asss_step.restype = ctypes.c_int
+    L.amh_asss_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, I32, P, P]
+    L.amh_asss_sample_pnx.restype = ctypes.c_int
     for name in EXPORTS[:10]:
         getattr(L, name).restype = ctypes.c_int if name != "amh_last_error" else ctypes.c_char_p
     _lib = L

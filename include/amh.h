@@ -130,6 +130,26 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
 int amh_chain_keys(const uint32_t key[2], int64_t chain_offset, int64_t n, uint32_t* out,
                    void* stream);
 
+/* ------------------------------------------------------------------ ASSS ----
+ * asss.py:197-251 (ASSS.sample) applied n_steps times to every chain: the
+ * adaptive stereographic slice sampler with the same adaptation as ARWMH
+ * (mean, rank-one Cholesky update, NaN -> keep L) and as_change =
+ * ||mu' - mu|| + ||L' - L||_F.  Uses i, z, potential_energy, loc, scale,
+ * as_change and rng_key of the states (mean_accept_prob / log_step_size are
+ * not read or written and may be NULL).  Initial states come from amh_init
+ * (asss.py:134-189 equals arwmh.py:84-138 on these leaves).  d <= 64.
+ * `in` and `out` may alias.  collect: as amh_step (z / potential_energy). */
+int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+                  int32_t n_steps, const amh_collect* collect, void* stream);
+
+/* asss.py:271-303 (ASSS.sample_Pnx): n transitions with the frozen shared
+ * adapt state (loc[d], scale_packed[P]) from every x[pt] for n_samples chains
+ * each; out: device [n_points][n_samples][d].  Chain keys as amh_sample_pnx;
+ * transition t draws at stream position t.  key[2] in host memory. */
+int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t n_points,
+                        int64_t n_samples, const float* loc, const float* scale_packed, int32_t n,
+                        float* out, void* stream);
+
 /* ---------------------------------------------------- pooled covariance ----
  * Regime B (build-defined, no reference analogue): every chain
  * proposes with ONE shared adapt state, and the adaptation of arwmh.py:180-197

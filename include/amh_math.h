@@ -78,6 +78,8 @@ AMH_HD amh_u32x4 amh_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32
 #define AMH_TAG_INIT     0x54494E49u /* init_to_uniform draws                 */
 #define AMH_TAG_STEP     0x50455453u /* per-step proposal / accept draws      */
 #define AMH_TAG_SPLIT    0x54494C50u /* key splitting (sample_Pnx keys)       */
+#define AMH_TAG_ASSS     0x53535341u /* ASSS per-step draws (c2 = 0: v, u_t,
+                                        theta_0; c2 = 1: shrink uniforms)   */
 
 /* 32 random bits -> float in [0,1): jax.random.uniform's construction
  * (mantissa fill of [1,2) then subtract 1). */
@@ -195,6 +197,33 @@ AMH_HD float amh_normal_from_bits(uint32_t b) {
   float u = (f * 2.0f) + lo;     /* (hi - lo) rounds to 2 in fp32 */
   u = (u < lo) ? lo : u;
   return 1.41421356f * amh_erfinvf(u);
+}
+
+/* ----------------------------------------------------------- sin/cos ---- */
+/* Cephes-style single precision sin and cos of one argument (the slice
+ * angle of ASSS, asss.py:69, :95: |theta| < 2 pi).  theta = k pi/2 + r with
+ * k = rint(theta 2/pi) and a three-part Cody-Waite reduction (fmaf), then the
+ * sinf / cosf minimax polynomials on |r| <= pi/4 and the quadrant swap. */
+AMH_HD void amh_sincosf(float x, float* s_out, float* c_out) {
+  const float kf = rintf(x * 0.636619772367581343f);
+  const int k = (int)kf;
+  float r = fmaf(kf, -1.57079637050628662109375f, x);
+  r = fmaf(kf, 4.37113882867379e-08f, r);
+  r = fmaf(kf, 1.7151245100059596e-15f, r);
+  const float z = r * r;
+  float ps = -1.9515295891e-4f;
+  ps = fmaf(ps, z, 8.3321608736e-3f);
+  ps = fmaf(ps, z, -1.6666654611e-1f);
+  const float sr = fmaf(ps * z, r, r);
+  float pc = 2.443315711809948e-5f;
+  pc = fmaf(pc, z, -1.388731625493765e-3f);
+  pc = fmaf(pc, z, 4.166664568298827e-2f);
+  const float cr = fmaf(pc * z, z, fmaf(-0.5f, z, 1.0f));
+  const int q = k & 3;
+  const float s = (q == 0) ? sr : ((q == 1) ? cr : ((q == 2) ? -sr : -cr));
+  const float c = (q == 0) ? cr : ((q == 1) ? -sr : ((q == 2) ? -cr : sr));
+  *s_out = s;
+  *c_out = c;
 }
 
 /* ------------------------------------------------- double log/exp/pow ---- */

@@ -1161,3 +1161,268 @@ static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t
   *lam = lamn;
   return ok;
 }
+
+/* ================================================================= ASSS ==== */
+/* asss.py:197-251 (ASSS.sample), kernel mirror of amh_asss.hip: the chain is
+ * held as (U, dl) between the steps of one launch like chain_t; the factor
+ * is written back as U diag(dl) if any step updated it, else verbatim.
+ * Noise at stream position i: v_r = N(Philox(r, i, 0)[0]); v_d, u_t, th_0
+ * from words 1-3 of Philox(0, i, 0); shrink step k: U(Philox(k, i, 1)[0]). */
+static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, int adapt) {
+  const int d = cfg->d;
+  const int G = orc_gw(cfg);
+  const uint32_t it = (uint32_t)s->i;
+  const float sd = sqrtf((float)d);
+  const float epsd = cfg->eps * sd;
+  const float fd = (float)d;
+  /* draws (asss.py:207, 219, 225, 60) */
+  float v[ORC_DMAX];
+  uint32_t w1 = 0, w2 = 0, w3 = 0;
+  for (int r = 0; r < d; ++r) {
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, it, 0u, AMH_TAG_ASSS, k0, k1);
+    v[r] = amh_normal_from_bits(o.v[0]);
+    if (r == 0) { w1 = o.v[1]; w2 = o.v[2]; w3 = o.v[3]; }
+  }
+  float vd = amh_normal_from_bits(w1);
+  const float ut = amh_unif01_from_bits(w2);
+  const float th0 = 6.28318548f * amh_unif01_from_bits(w3);
+  /* y = S^-1 (x - mu), S = (L + eps I) sqrt(d): S_rj = U_rj e_j, S_rr = D_r */
+  float e[ORC_DMAX], invD[ORC_DMAX], b[ORC_DMAX], y[ORC_DMAX];
+  for (int r = 0; r < d; ++r) {
+    e[r] = s->dl[r] * sd;
+    invD[r] = 1.0f / ((s->dl[r] + cfg->eps) * sd);
+    b[r] = s->z[r] - s->mu[r];
+  }
+  for (int j = 0; j < d; ++j) {
+    const float yj = b[j] * invD[j];
+    y[j] = yj;
+    const float gj = yj * e[j];
+    for (int r = 0; r < d; ++r) b[r] = fmaf(-s->U[r][j], gj, b[r]);
+  }
+  /* stereographic projection (asss.py:40-45) */
+  float t[ORC_DMAX];
+  for (int r = 0; r < G; ++r) t[r] = (r < d) ? y[r] * y[r] : 0.0f;
+  const float ns = group_sum(t, G);
+  const float den = ns + 1.0f;
+  float zr[ORC_DMAX];
+  for (int r = 0; r < d; ++r) zr[r] = (2.0f * y[r]) / den;
+  const float zd = (ns - 1.0f) / den;
+  /* v on the tangent space of z, normalised (asss.py:219-222) */
+  for (int r = 0; r < G; ++r) t[r] = (r < d) ? v[r] * zr[r] : 0.0f;
+  const float dot = group_sum(t, G) + (vd * zd);
+  for (int r = 0; r < d; ++r) v[r] = v[r] - dot * zr[r];
+  vd = vd - dot * zd;
+  for (int r = 0; r < G; ++r) t[r] = (r < d) ? v[r] * v[r] : 0.0f;
+  const float nv = sqrtf(group_sum(t, G) + (vd * vd));
+  for (int r = 0; r < d; ++r) v[r] = v[r] / nv;
+  vd = vd / nv;
+  /* S z_1d and S v_1d */
+  float Sz[ORC_DMAX], Sv[ORC_DMAX], hz[ORC_DMAX], hv[ORC_DMAX];
+  for (int j = 0; j < d; ++j) { hz[j] = e[j] * zr[j]; hv[j] = e[j] * v[j]; }
+  for (int r = 0; r < d; ++r) {
+    float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, c4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    for (int j = 0; j < d; ++j) {
+      a4[j & 3] = fmaf(s->U[r][j], hz[j], a4[j & 3]);
+      c4[j & 3] = fmaf(s->U[r][j], hv[j], c4[j & 3]);
+    }
+    Sz[r] = ((a4[0] + a4[1]) + (a4[2] + a4[3])) + epsd * zr[r];
+    Sv[r] = ((c4[0] + c4[1]) + (c4[2] + c4[3])) + epsd * v[r];
+  }
+  /* slice level at z (asss.py:216-217, 224-226) */
+  float x0[ORC_DMAX], xt[ORC_DMAX];
+  float om0;
+  {
+    const float zdt = (zd * 1.0f) + (vd * 0.0f);
+    om0 = 1.0f - zdt;
+    for (int r = 0; r < d; ++r) x0[r] = (((Sz[r] * 1.0f) + (Sv[r] * 0.0f)) / om0) + s->mu[r];
+  }
+  const float U0 = orc_potential1(cfg, x0);
+  const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
+  /* shrinkage (asss.py:59-96) */
+  float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
+  int iter = 0;
+  float ux;
+  int cont;
+  {
+    float sn, cs;
+    amh_sincosf(th, &sn, &cs);
+    const float om = 1.0f - ((zd * cs) + (vd * sn));
+    for (int r = 0; r < d; ++r) xt[r] = (((Sz[r] * cs) + (Sv[r] * sn)) / om) + s->mu[r];
+    ux = orc_potential1(cfg, xt);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    cont = (pt > tpe) || (om < cfg->eps);
+  }
+  while (cont) {
+    if (th < 0.0f) thmin = th;
+    if (th >= 0.0f) thmax = th;
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)iter, it, 1u, AMH_TAG_ASSS, k0, k1);
+    th = thmin + (thmax - thmin) * amh_unif01_from_bits(o.v[0]);
+    float sn, cs;
+    amh_sincosf(th, &sn, &cs);
+    const float om = 1.0f - ((zd * cs) + (vd * sn));
+    for (int r = 0; r < d; ++r) xt[r] = (((Sz[r] * cs) + (Sv[r] * sn)) / om) + s->mu[r];
+    ux = orc_potential1(cfg, xt);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    iter += 1;
+    cont = (iter < 50) && ((pt > tpe) || (om < cfg->eps));
+  }
+  const int capped = iter >= 50;
+  float xn[ORC_DMAX];
+  for (int r = 0; r < d; ++r) xn[r] = capped ? x0[r] : xt[r];
+  float pen = capped ? U0 : ux;
+  if (amh_isnan(pen)) pen = INFINITY;
+  if (!adapt) { /* frozen kernel (sample_Pnx) */
+    for (int r = 0; r < d; ++r) s->z[r] = xn[r];
+    s->pe = pen;
+    return;
+  }
+  /* adaptation (asss.py:237-251) */
+  const int32_t itr = s->i + 1;
+  const int32_t n = (s->i < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  float delta[ORC_DMAX], mun[ORC_DMAX];
+  for (int r = 0; r < G; ++r) t[r] = 0.0f;
+  for (int r = 0; r < d; ++r) {
+    delta[r] = xn[r] - s->mu[r];
+    mun[r] = s->mu[r] + gamma * delta[r];
+    const float dm = mun[r] - s->mu[r];
+    t[r] = dm * dm;
+  }
+  const float locd = sqrtf(group_sum(t, G));
+  const float sq = sqrtf(1.0f - gamma);
+  float Dg[ORC_DMAX], one[ORC_DMAX];
+  for (int j = 0; j < d; ++j) {
+    const float ajj = sq * s->dl[j];
+    Dg[j] = ajj * ajj;
+    one[j] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : NAN;
+  }
+  float w[ORC_DMAX], ws[ORC_DMAX];
+  for (int r = 0; r < d; ++r) w[r] = delta[r];
+  for (int j = 0; j < d; ++j) {
+    const float wj = w[j];
+    ws[j] = wj;
+    for (int r = 0; r < d; ++r) w[r] = fmaf(-wj, s->U[r][j], w[r]);
+  }
+  float tsc[ORC_DMAX], bsc[ORC_DMAX], cc[ORC_DMAX], qq[ORC_DMAX], gw2[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    gw2[r] = (r < d) ? gamma * (ws[r] * ws[r]) : 0.0f;
+    tsc[r] = (r < d) ? gw2[r] / Dg[r] : 0.0f;
+  }
+  group_excl_scan(tsc, bsc, G);
+  int revert = 0;
+  for (int r = 0; r < d; ++r) {
+    const float bb = 1.0f + bsc[r];
+    const float g2 = (bb * Dg[r]) + gw2[r];
+    const float dn = g2 / bb;
+    cc[r] = (gamma * ws[r]) / g2;
+    qq[r] = sqrtf(dn);
+    revert |= amh_isnan(fmaf(cc[r], 0.0f, one[r]) * qq[r]);
+  }
+  float sdiff = 0.0f;
+  if (!revert) {
+    float ac[ORC_DMAX], bc[ORC_DMAX], s4[ORC_DMAX][4];
+    for (int r = 0; r < d; ++r) {
+      ac[r] = qq[r] - s->dl[r];
+      bc[r] = cc[r] * qq[r];
+      s4[r][0] = s4[r][1] = s4[r][2] = s4[r][3] = 0.0f;
+      w[r] = delta[r];
+    }
+    for (int j = 0; j < d; ++j)
+      for (int r = 0; r < d; ++r) {
+        const float uo = s->U[r][j];
+        w[r] = fmaf(-ws[j], uo, w[r]);
+        const float un = fmaf(cc[j], w[r], uo);
+        const float tt = fmaf(uo, ac[j], bc[j] * w[r]);
+        s4[r][j & 3] = fmaf(tt, tt, s4[r][j & 3]);
+        s->U[r][j] = un;
+      }
+    for (int r = 0; r < G; ++r) t[r] = (r < d) ? (s4[r][0] + s4[r][1]) + (s4[r][2] + s4[r][3]) : 0.0f;
+    sdiff = sqrtf(group_sum(t, G));
+    for (int r = 0; r < d; ++r) s->dl[r] = qq[r];
+    s->updated = 1;
+  }
+  s->asc = locd + sdiff;
+  s->i = itr;
+  for (int r = 0; r < d; ++r) { s->z[r] = xn[r]; s->mu[r] = mun[r]; }
+  s->pe = pen;
+}
+
+/* n_steps ASSS transitions of chains [0, C) in place (one kernel launch);
+ * collect_z [n_steps][C][d] / collect_pe [n_steps][C] nullable. */
+void orc_asss_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe, float* mu,
+                   float* L, float* asc, const uint32_t* keys, float* collect_z, float* collect_pe) {
+  const int d = cfg->d;
+  if (d > ORC_DMAX) return;
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t c = 0; c < C; ++c) {
+    chain_t* s = (chain_t*)malloc(sizeof(chain_t));
+    const float* Lc = L + c * packed_size(d);
+    float inv[ORC_DMAX];
+    for (int r = 0; r < d; ++r) {
+      s->dl[r] = Lc[col_off(d, r)];
+      inv[r] = (amh_isfinite(s->dl[r]) && s->dl[r] != 0.0f) ? 1.0f / s->dl[r] : 0.0f;
+    }
+    for (int r = 0; r < d; ++r)
+      for (int j = 0; j < d; ++j) {
+        const float x = (r > j) ? Lc[col_off(d, j) + (r - j)] : 0.0f;
+        s->U[r][j] = (r == j) ? 1.0f : x * inv[j];
+      }
+    for (int r = 0; r < d; ++r) { s->z[r] = z[c * d + r]; s->mu[r] = mu[c * d + r]; }
+    s->i = i_[c];
+    s->pe = pe[c];
+    s->asc = asc[c];
+    s->updated = 0;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      asss_chain_step(cfg, s, keys[2 * c], keys[2 * c + 1], 1);
+      if (collect_z)
+        for (int r = 0; r < d; ++r) collect_z[((int64_t)t * C + c) * d + r] = s->z[r];
+      if (collect_pe) collect_pe[(int64_t)t * C + c] = s->pe;
+    }
+    if (s->updated) {
+      float* Lw = L + c * packed_size(d);
+      for (int j = 0; j < d; ++j)
+        for (int r = j; r < d; ++r) Lw[col_off(d, j) + (r - j)] = s->U[r][j] * s->dl[j];
+    }
+    for (int r = 0; r < d; ++r) { z[c * d + r] = s->z[r]; mu[c * d + r] = s->mu[r]; }
+    i_[c] = s->i;
+    pe[c] = s->pe;
+    asc[c] = s->asc;
+    free(s);
+  }
+}
+
+/* asss.py:271-303 (ASSS.sample_Pnx), mirror of asss_pnx_kernel: chain
+ * c = (p, s) starts at x[p] with key split(key, C)[c], frozen shared
+ * (loc, L); transition t at stream position t. */
+void orc_asss_sample_pnx(const orc_cfg* cfg, const uint32_t* key, const float* x, int64_t n_points,
+                         int64_t n_samples, const float* loc, const float* Lpacked, int32_t n, float* out) {
+  const int d = cfg->d;
+  const int64_t C = n_points * n_samples;
+#pragma omp parallel for schedule(dynamic, 64)
+  for (int64_t c = 0; c < C; ++c) {
+    chain_t* s = (chain_t*)malloc(sizeof(chain_t));
+    float inv[ORC_DMAX];
+    for (int r = 0; r < d; ++r) {
+      s->dl[r] = Lpacked[col_off(d, r)];
+      inv[r] = (amh_isfinite(s->dl[r]) && s->dl[r] != 0.0f) ? 1.0f / s->dl[r] : 0.0f;
+    }
+    for (int r = 0; r < d; ++r)
+      for (int j = 0; j < d; ++j) {
+        const float xx = (r > j) ? Lpacked[col_off(d, j) + (r - j)] : 0.0f;
+        s->U[r][j] = (r == j) ? 1.0f : xx * inv[j];
+      }
+    const int64_t p = c / n_samples;
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, key[0],
+                                           key[1]);
+    for (int r = 0; r < d; ++r) { s->z[r] = x[p * d + r]; s->mu[r] = loc[r]; }
+    s->pe = orc_potential1(cfg, s->z);
+    for (int32_t t = 0; t < n; ++t) {
+      s->i = t;
+      asss_chain_step(cfg, s, kk.v[0], kk.v[1], 0);
+    }
+    for (int r = 0; r < d; ++r) out[c * d + r] = s->z[r];
+    free(s);
+  }
+}

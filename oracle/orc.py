@@ -71,6 +71,10 @@ def lib():
         L.orc_normal_bits.argtypes = [_P, _P, _I64]
         L.orc_lr_gamma.argtypes = [_P, _F, _P, _I64]
         L.orc_num_threads.restype = ctypes.c_int
+        L.orc_asss_step.argtypes = [_P, _I64, _I32] + [_P] * 9
+        L.orc_asss_step.restype = None
+        L.orc_asss_sample_pnx.argtypes = [_P, _P, _P, _I64, _I64, _P, _P, _I32, _P]
+        L.orc_asss_sample_pnx.restype = None
         L.orc_pooled_cpw.argtypes = [_I64]
         L.orc_pooled_cpw.restype = ctypes.c_int
         L.orc_pooled_stats.argtypes = [_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _P, _P, _P]
@@ -204,6 +208,30 @@ def step(model: Model, state: State, n_steps: int = 1, num_warmup: int = 0, lr_d
                    _ptr(state.mean_accept_prob), _ptr(state.loc), _ptr(state.scale), _ptr(state.log_step_size),
                    _ptr(state.as_change), _ptr(state.rng_key), _ptr(accept_count), _ptr(cz))
     return cz
+
+
+def asss_step(model: Model, state: State, n_steps: int = 1, num_warmup: int = 0, lr_decay: float = 2 / 3,
+              eps: float = 1e-6, collect_z=False, collect_pe=False):
+    """ASSS transitions (asss.py:197-251) in place, one launch; the state's
+    mean_accept_prob / log_step_size are not touched.  Returns (cz, cp)."""
+    C = state.z.shape[0]
+    cfg = model.cfg(num_warmup, lr_decay, 0.234, eps)
+    cz = np.empty((n_steps, C, model.d), np.float32) if collect_z else None
+    cp = np.empty((n_steps, C), np.float32) if collect_pe else None
+    lib().orc_asss_step(ctypes.byref(cfg), C, n_steps, _ptr(state.i), _ptr(state.z), _ptr(state.potential_energy),
+                        _ptr(state.loc), _ptr(state.scale), _ptr(state.as_change), _ptr(state.rng_key), _ptr(cz),
+                        _ptr(cp))
+    return cz, cp
+
+
+def asss_sample_pnx(model: Model, key, x: np.ndarray, loc, scale_packed, n: int, n_samples: int,
+                    eps: float = 1e-6) -> np.ndarray:
+    x = _c(x, np.float32).reshape(-1, model.d)
+    out = np.empty((x.shape[0], n_samples, model.d), np.float32)
+    cfg = model.cfg(0, 2 / 3, 0.234, eps)
+    lib().orc_asss_sample_pnx(ctypes.byref(cfg), _ptr(_c(key, np.uint32)), _ptr(x), x.shape[0], n_samples,
+                              _ptr(_c(loc, np.float32)), _ptr(_c(scale_packed, np.float32)), n, _ptr(out))
+    return out
 
 
 def sample_pnx(model: Model, key, x: np.ndarray, loc, scale_packed, log_step_size: float, n: int,

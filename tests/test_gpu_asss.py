@@ -1,0 +1,116 @@
+"""GPU parity for ASSS (amh_asss.hip through the C ABI, via kernels.ASSS)
+against the C oracle's mirror (orc_asss_step / orc_asss_sample_pnx): every
+float of every state field, bit for bit; plus the eight-schools posterior the
+reference notebook prints for ASSS (posteriordb_eight-schools.ipynb cell 29)."""
+import numpy as np
+import pytest
+import torch
+
+from helpers import make_case
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("i", "z", "potential_energy", "loc", "scale", "as_change", "rng_key")
+
+
+def _gpu_fields(s):
+    a = s.adapt_state
+    return dict(i=s.i, z=s.z, potential_energy=s.potential_energy, loc=a.loc, scale=a.scale,
+                as_change=s.as_change, rng_key=s.rng_key)
+
+
+def assert_bitequal(st, ost, what):
+    g = _gpu_fields(st)
+    for f in FIELDS:
+        a = g[f].cpu().numpy()
+        b = np.asarray(getattr(ost, f))
+        av = a.view(np.uint32)
+        bv = b.astype(a.dtype).view(np.uint32) if b.dtype != a.dtype and f != "rng_key" else b.view(np.uint32)
+        bad = np.flatnonzero((av != bv).reshape(-1))
+        assert bad.size == 0, (f"{what}: {f} differs in {bad.size} of {av.size}; first {bad[:4]}: "
+                               f"gpu {a.reshape(-1)[bad[:4]]} oracle {b.reshape(-1)[bad[:4]]}")
+
+
+def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
+    from kernels import ASSS, PRNGKey
+    kw, mk, om = make_case(kind, d)
+    k = ASSS(num_chains=C, **kw)
+    key = PRNGKey(seed)
+    if "potential_fn" in kw:
+        z0 = np.random.default_rng(seed).uniform(-2, 2, size=(C, om.d)).astype(np.float32)
+        st = k.init(key, num_warmup, torch.as_tensor(z0), (), mk)
+        ost = orc.init(om, key, C, init_z=z0)
+    else:
+        st = k.init(key, num_warmup, None, (), mk)
+        ost = orc.init(om, key, C)
+    torch.cuda.synchronize()
+    return k, st, om, ost
+
+
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 600), ("gaussian", 5, 517), ("gaussian", 16, 300),
+                                      ("gaussian", 33, 130), ("eight_schools", None, 400), ("kidiq", None, 257),
+                                      ("diamonds", None, 66)])
+def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
+    """ASSS.sample (one launch per step, out of place) vs oracle, 25 steps."""
+    k, st, om, ost = _init(kind, C, orc, d=d, num_warmup=8)
+    assert_bitequal(st, ost, f"{kind} init")
+    for t in range(25):
+        st = k.sample(st, (), {})
+        orc.asss_step(om, ost, 1, num_warmup=8)
+        torch.cuda.synchronize()
+        assert_bitequal(st, ost, f"{kind} step {t}")
+
+
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("eight_schools", None, 700), ("diamonds", None, 40)])
+def test_asss_fused_and_collect_bitexact(kind, d, C, gpu, orc):
+    """ASSS.run (n steps per launch, z / pe collected with thinning) and the
+    in-place ASSS.sample_ vs the oracle's launch-for-launch mirror."""
+    k, st, om, ost = _init(kind, C, orc, d=d)
+    for n in (1, 6, 40):
+        st, cz, cp = k.run(st, n, thinning=2, collect_z=True, collect_pe=True)
+        ocz, ocp = orc.asss_step(om, ost, n, collect_z=True, collect_pe=True)
+        torch.cuda.synchronize()
+        assert_bitequal(st, ost, f"{kind} fused {n}")
+        if n >= 2:
+            np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), ocz[1::2][: n // 2].view(np.uint32))
+            np.testing.assert_array_equal(cp.cpu().numpy().view(np.uint32), ocp[1::2][: n // 2].view(np.uint32))
+    k.sample_(st, 9)
+    orc.asss_step(om, ost, 9)
+    torch.cuda.synchronize()
+    assert_bitequal(st, ost, f"{kind} in place")
+
+
+def test_asss_sample_pnx_bitexact(gpu, orc):
+    from kernels import PRNGKey
+    k, st, om, ost = _init("eight_schools", 64, orc)
+    k.sample_(st, 300)
+    a = st.adapt_state
+    loc, scale = a.loc[3].clone(), a.scale[3].clone()
+    x = st.z[:5].clone()
+    out = k.sample_Pnx(PRNGKey(9), x, (loc, scale), n=4, n_samples=37)
+    ref = orc.asss_sample_pnx(om, PRNGKey(9), x.cpu().numpy(), loc.cpu().numpy(), scale.cpu().numpy(), 4, 37)
+    assert out.shape == (5, 37, om.d)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_asss_eight_schools_posterior(gpu):
+    """Notebook cell 29 (ASSS, 2.5e4 warmup, 2.5e5 samples, thinning 25):
+    mu 4.46 (sd 3.30), tau 3.54 (3.20), theta_base[0] 0.31 (0.98); on 256
+    chains (2.56M kept draws) through infer.MCMC."""
+    import posteriors as P
+    from infer import MCMC
+    from kernels import ASSS, PRNGKey
+    k = ASSS(model=P.eight_schools, num_chains=256)
+    m = MCMC(k, num_warmup=25000, num_samples=250000, thinning=25)
+    m.run(PRNGKey(0), extra_fields=("potential_energy",), **P.EIGHT_SCHOOLS_DATA)
+    s = m.get_samples()
+    assert s["mu"].shape == (256 * 10000,)
+    assert float(s["mu"].mean()) == pytest.approx(4.46, abs=0.1)
+    assert float(s["mu"].std()) == pytest.approx(3.30, abs=0.1)
+    assert float(s["tau"].mean()) == pytest.approx(3.54, abs=0.12)
+    assert float(s["tau"].std()) == pytest.approx(3.20, abs=0.12)
+    assert float(s["theta_base"][:, 0].mean()) == pytest.approx(0.31, abs=0.03)
+    assert float(s["theta_base"][:, 0].std()) == pytest.approx(0.98, abs=0.04)
+    # notebook min U 41.17 over 1e4 draws; the minimum over 2.56M draws sits lower
+    assert 39.5 < float(m.get_extra_fields()["potential_energy"].min()) < 41.5
+    assert "Iteration: 275000" in k.get_diagnostics_str(m.last_state)
