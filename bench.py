@@ -34,7 +34,7 @@ def bytes_per_chain_step(d: int) -> int:
     return 2 * 4 * (d * (d + 1) // 2 + 2 * d + 6)
 
 
-def ess(x: np.ndarray) -> float:
+def ess_of(x: np.ndarray) -> float:
     """Multi-chain ESS of x [chains, draws] (numpyro's estimator, the n_eff
     of print_summary: adaptive-mcmc_amd/infer/diagnostics.py)."""
     from infer.diagnostics import effective_sample_size
@@ -200,8 +200,8 @@ def main():
         el = time.perf_counter() - e0
         zc = cz.cpu().numpy()
         pc = cp.cpu().numpy()
-        vals = [ess(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
-        vals.append(ess(pc.T.astype(np.float64)))
+        vals = [ess_of(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
+        vals.append(ess_of(pc.T.astype(np.float64)))
         ess = {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T,
                "seconds": el, "coords": [0, 1, d // 2, d - 1, "U"]}
 

@@ -51,18 +51,18 @@ def run_regime_a(name, kernel, C, d, kwargs, steps, warmup, dev):
     fused = C * 10 / (time.perf_counter() - f0)
     return {"config": name, "chains": C, "dim": d, "steps": steps, "value": C * steps / wall,
             "unit": "chain-steps/s", "kernel_ms": kms, "fused_chain_steps_per_s": fused,
-            "mean_accept_prob": float(st.mean_accept_prob.mean())}
+            "mean_accept_prob": float(st.mean_accept_prob.mean()) if hasattr(st, "mean_accept_prob") else None}
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64")
+    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64,asss64,asss_es")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
     import torch
     import posteriors as P
-    from kernels import ARWMH, PooledARWMH, PRNGKey
+    from kernels import ARWMH, ASSS, PooledARWMH, PRNGKey
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     want = set(args.only.split(","))
@@ -78,6 +78,17 @@ def main():
         k = ARWMH(potential_fn=g, num_chains=C, device=dev)
         print(json.dumps(run_regime_a("gauss256 regime A (BASELINE configs[3])", k, C, 256, {},
                                       args.steps, args.warmup, dev)), flush=True)
+    if "asss64" in want:
+        g = P.correlated_gaussian(64)
+        C = 65536
+        k = ASSS(potential_fn=g, num_chains=C, device=dev)
+        print(json.dumps(run_regime_a("ASSS d=64 correlated Gaussian", k, C, 64, {}, args.steps, args.warmup, dev)),
+              flush=True)
+    if "asss_es" in want:
+        C = 262144
+        k = ASSS(model=P.eight_schools, num_chains=C, device=dev)
+        print(json.dumps(run_regime_a("ASSS eight schools", k, C, 10, dict(P.EIGHT_SCHOOLS_DATA), args.steps,
+                                      args.warmup, dev)), flush=True)
     for key, d, C, kappa in (("gauss256_pooled", 256, 32768, 4.0), ("pooled64", 64, 65536, 2.0)):
         if key not in want:
             continue
