@@ -259,10 +259,10 @@ __global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p)
   const float mun = act ? p.in.loc[r] + gamma * (float)(sums[r] / N) : 0.0f;
   const double g = (double)gamma;
 
-  // Sigma' (double) in LDS, row r written by lane r; the old factor's row in
-  // registers.  Every lane loads a valid element (index 0 off the triangle)
-  // so the loads are not serialised behind divergent branches.
-  __shared__ double As[64][65];
+  // Sigma' (double) row r in lane r's registers, the old factor's row too.
+  // Every lane loads a valid element (index 0 off the triangle) so the loads
+  // are not serialised behind divergent branches.
+  double A[64];
   float Lo[64];
   static_for<64>([&](auto K) {
     constexpr int k = K;
@@ -273,30 +273,39 @@ __global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p)
     const float lv = p.in.scale[o];
     const double a = (1.0 - g) * cv;
     const double b = g * (sv / N);
-    As[r][k] = in ? a + b : 0.0;
+    A[k] = in ? a + b : 0.0;
     Lo[k] = in ? lv : 0.0f;
   });
-  // Right-looking Cholesky in LDS, lane r = row r: element (r, k) is updated
-  // in column order with fma(-L_rj, L_kj, A_rk) (oracle mirror).
+  // Right-looking Cholesky, lane r = row r, in registers: element (r, k) is
+  // updated in column order with fma(-L_rj, L_kj, A_rk) (oracle mirror).
+  // Column j goes through LDS once and is read back as 16-B broadcasts; the
+  // entries above the diagonal are updated too (never used), so no lane masks.
+  __shared__ __attribute__((aligned(16))) double colb[64];
   bool ok = true;
-  for (int j = 0; j < d; ++j) {
-    const double piv = As[j][j];
-    ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
-    const double ljj = sqrt(piv);
-    double lrj = 0.0;
-    if (r > j && act) {
-      lrj = As[r][j] / ljj;
-      As[r][j] = lrj;
+  static_for<64>([&](auto J) {
+    constexpr int j = J;
+    if (j < d) {
+      const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(A[j]), j),
+                                          __builtin_amdgcn_readlane(__double2loint(A[j]), j));
+      ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
+      const double ljj = sqrt(piv);
+      const double lrj = A[j] / ljj;
+      A[j] = (r == j) ? ljj : lrj;
+      colb[r] = lrj;
+      static_for<(64 - ((j + 1) & ~1)) / 2>([&](auto Q) {
+        constexpr int k0 = ((j + 1) & ~1) + 2 * Q;
+        if (k0 < d) {
+          typedef double f64x2 __attribute__((ext_vector_type(2)));
+          const f64x2 v = *(const f64x2*)&colb[k0];
+          if constexpr (k0 > j) A[k0] = fma(-lrj, v[0], A[k0]);
+          if constexpr (k0 + 1 > j) {
+            if (k0 + 1 < d) A[k0 + 1] = fma(-lrj, v[1], A[k0 + 1]);
+          }
+        }
+      });
+      asm volatile("" ::: "memory");
     }
-    if (r == j) As[j][j] = ljj;
-#pragma unroll 4
-    for (int k = j + 1; k < d; ++k) {
-      const double lkj = As[k][j];
-      if (r >= k && act) As[r][k] = fma(-lrj, lkj, As[r][k]);
-    }
-  }
-  double A[64];
-  static_for<64>([&](auto K) { A[K] = As[r][K]; });
+  });
   const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
   float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
   static_for<64>([&](auto J) {
