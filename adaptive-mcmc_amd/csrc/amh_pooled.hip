@@ -238,12 +238,17 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
 }
 }  // namespace
 
-// One wave: lane r holds row r of Sigma' (double) and factors it in place
-// (right-looking; element (r, k) is updated in column order, oracle mirror).
-__global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p) {
+// 8 waves move the packed matrices between HBM and LDS with coalesced
+// column accesses; wave 0 holds row r of Sigma' (double) in lane r and
+// factors it in registers (right-looking; element (r, k) is updated in column
+// order, oracle mirror).
+constexpr int kUpdLd = 65;  // LDS row stride of the [r][k] staging arrays
+
+__global__ __launch_bounds__(512) void pooled_update_kernel(PooledUpdateParams p) {
   const int d = p.d;
-  const int r = lane_id();
-  const bool act = r < d;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane(tid / 64);
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const double* sums = p.sums;
   const double N = sums[d + P + 1];
@@ -251,98 +256,114 @@ __global__ __launch_bounds__(64) void pooled_update_kernel(PooledUpdateParams p)
   const int32_t itr = it + 1;
   const int32_t n = (it < p.W) ? itr : itr - p.W;
   const float gamma = amh_lr_gamma(n, p.a);
-  const float macc = p.in.mean_accept_prob[0];
-  const float lam = p.in.log_step_size[0];
-  const float abar = (float)(sums[d + P] / N);
-  const float maccn = macc + (abar - macc) / (float)n;
-  const float lamn = lam + gamma * (abar - p.target);
-  const float mun = act ? p.in.loc[r] + gamma * (float)(sums[r] / N) : 0.0f;
   const double g = (double)gamma;
+  __shared__ double As[64 * kUpdLd];  // Sigma' [r][k], then the new factor (float view)
+  __shared__ float Los[64 * kUpdLd];  // old factor [r][k]
+  __shared__ int okv;
 
-  // Sigma' (double) row r in lane r's registers, the old factor's row too.
-  // Every lane loads a valid element (index 0 off the triangle) so the loads
-  // are not serialised behind divergent branches.
-  double A[64];
-  float Lo[64];
-  static_for<64>([&](auto K) {
-    constexpr int k = K;
-    const bool in = k < d && act && k <= r;
-    const int64_t o = in ? col_off(d, k) + (r - k) : 0;
-    const double cv = p.in.cov[o];
-    const double sv = sums[d + o];
-    const float lv = p.in.scale[o];
-    const double a = (1.0 - g) * cv;
-    const double b = g * (sv / N);
-    A[k] = in ? a + b : 0.0;
-    Lo[k] = in ? lv : 0.0f;
-  });
-  // Right-looking Cholesky, lane r = row r, in registers: element (r, k) is
-  // updated in column order with fma(-L_rj, L_kj, A_rk) (oracle mirror).
-  // Column j goes through LDS once and is read back as 16-B broadcasts; the
-  // entries above the diagonal are updated too (never used), so no lane masks.
-  __shared__ __attribute__((aligned(16))) double colb[64];
-  bool ok = true;
-  static_for<64>([&](auto J) {
-    constexpr int j = J;
-    if (j < d) {
-      const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(A[j]), j),
-                                          __builtin_amdgcn_readlane(__double2loint(A[j]), j));
-      ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
-      const double ljj = sqrt(piv);
-      const double lrj = A[j] / ljj;
-      A[j] = (r == j) ? ljj : lrj;
-      colb[r] = lrj;
-      static_for<(64 - ((j + 1) & ~1)) / 2>([&](auto Q) {
-        constexpr int k0 = ((j + 1) & ~1) + 2 * Q;
-        if (k0 < d) {
+  // (1) Sigma' = (1-g) Sigma + g S_dd / N and the old factor into LDS;
+  // wave w takes columns w, w + 8, ..; lane = row offset
+  for (int k = w; k < d; k += 8) {
+    const int r = k + lane;
+    if (r < d) {
+      const int64_t o = col_off(d, k) + (r - k);
+      const double a = (1.0 - g) * p.in.cov[o];
+      const double b = g * (sums[d + o] / N);
+      As[r * kUpdLd + k] = a + b;
+      Los[r * kUpdLd + k] = p.in.scale[o];
+    }
+  }
+  __syncthreads();
+
+  if (w == 0) {
+    const int r = lane;
+    const bool act = r < d;
+    const float macc = p.in.mean_accept_prob[0];
+    const float lam = p.in.log_step_size[0];
+    const float abar = (float)(sums[d + P] / N);
+    const float maccn = macc + (abar - macc) / (float)n;
+    const float lamn = lam + gamma * (abar - p.target);
+    const float mun = act ? p.in.loc[r] + gamma * (float)(sums[r] / N) : 0.0f;
+    double A[64];
+    static_for<64>([&](auto K) {
+      constexpr int k = K;
+      A[k] = (k < d && act && k <= r) ? As[r * kUpdLd + k] : 0.0;
+    });
+    // Right-looking Cholesky, lane r = row r, in registers.  Column j goes
+    // through LDS once and is read back as 16-B broadcasts; the entries above
+    // the diagonal are updated too (never used), so no lane masks.
+    __shared__ __attribute__((aligned(16))) double colb[64];
+    bool ok = true;
+    static_for<64>([&](auto J) {
+      constexpr int j = J;
+      if (j < d) {
+        const double piv = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(A[j]), j),
+                                            __builtin_amdgcn_readlane(__double2loint(A[j]), j));
+        ok = ok && (piv > 0.0) && __builtin_isfinite(piv);
+        const double ljj = sqrt(piv);
+        const double lrj = A[j] / ljj;
+        A[j] = (r == j) ? ljj : lrj;
+        colb[r] = lrj;
+        // columns k >= d are updated with garbage and never read: no branches
+        static_for<(64 - ((j + 1) & ~1)) / 2>([&](auto Q) {
+          constexpr int k0 = ((j + 1) & ~1) + 2 * Q;
           typedef double f64x2 __attribute__((ext_vector_type(2)));
           const f64x2 v = *(const f64x2*)&colb[k0];
           if constexpr (k0 > j) A[k0] = fma(-lrj, v[0], A[k0]);
-          if constexpr (k0 + 1 > j) {
-            if (k0 + 1 < d) A[k0 + 1] = fma(-lrj, v[1], A[k0 + 1]);
-          }
-        }
-      });
-      asm volatile("" ::: "memory");
-    }
-  });
-  const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
-  float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-  static_for<64>([&](auto J) {
-    constexpr int j = J;
-    if (j < d) {
-      const float lo = Lo[j];
-      const float ln = ok ? (float)A[j] : lo;
-      const float tt = (j <= r && act) ? (ln * e1) - (lo * e0) : 0.0f;
-      s4[j & 3] = fmaf(tt, tt, s4[j & 3]);
-    }
-  });
-  const float part = act ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0f;
-  const float asc = sqrtf(Grp<64>::sum(part));
-  // writes (each lane reads then writes only its own row: in-place safe)
-  if (act) {
-    static_for<64>([&](auto K) {
-      constexpr int k = K;
-      if (k < d && k <= r) {
-        const int64_t o = col_off(d, k) + (r - k);
-        if (ok) {
-          const double a = (1.0 - g) * p.in.cov[o];
-          const double b = g * (sums[d + o] / N);
-          p.out.cov[o] = a + b;
-          p.out.scale[o] = (float)A[k];
-        } else {  // kept (rare: gamma = 1 at n = 1, or Sigma' not positive definite)
-          p.out.cov[o] = p.in.cov[o];
-          p.out.scale[o] = Lo[k];
-        }
+          A[k0 + 1] = fma(-lrj, v[1], A[k0 + 1]);
+        });
+        asm volatile("" ::: "memory");
       }
     });
-    p.out.loc[r] = mun;
+    const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
+    float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float* Lns = (float*)As;  // the new factor, float [r][k] (row r's doubles are already in registers)
+    static_for<64>([&](auto J) {
+      constexpr int j = J;
+      if (j < d) {
+        const float lo = (j <= r && act) ? Los[r * kUpdLd + j] : 0.0f;
+        const float ln = ok ? (float)A[j] : lo;
+        const float tt = (j <= r && act) ? (ln * e1) - (lo * e0) : 0.0f;
+        s4[j & 3] = fmaf(tt, tt, s4[j & 3]);
+      }
+    });
+    const float part = act ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : 0.0f;
+    const float asc = sqrtf(Grp<64>::sum(part));
+    __builtin_amdgcn_s_waitcnt(0);
+    __builtin_amdgcn_wave_barrier();
+    static_for<64>([&](auto K) {
+      constexpr int k = K;
+      if (k < d && act && k <= r) Lns[r * kUpdLd + k] = (float)A[k];
+    });
+    if (act) p.out.loc[r] = mun;
+    if (r == 0) {
+      okv = ok ? 1 : 0;
+      p.out.i[0] = itr;
+      p.out.mean_accept_prob[0] = maccn;
+      p.out.log_step_size[0] = lamn;
+      p.out.as_change[0] = asc;
+    }
   }
-  if (r == 0) {
-    p.out.i[0] = itr;
-    p.out.mean_accept_prob[0] = maccn;
-    p.out.log_step_size[0] = lamn;
-    p.out.as_change[0] = asc;
+  __syncthreads();
+
+  // (3) write-out by column (in-place safe: every element is read and written
+  // by the same thread)
+  const bool ok = okv != 0;
+  const float* Lns = (const float*)As;
+  for (int k = w; k < d; k += 8) {
+    const int r = k + lane;
+    if (r < d) {
+      const int64_t o = col_off(d, k) + (r - k);
+      if (ok) {
+        const double a = (1.0 - g) * p.in.cov[o];
+        const double b = g * (sums[d + o] / N);
+        p.out.cov[o] = a + b;
+        p.out.scale[o] = Lns[r * kUpdLd + k];
+      } else {  // kept (rare: gamma = 1 at n = 1, or Sigma' not positive definite)
+        p.out.cov[o] = p.in.cov[o];
+        p.out.scale[o] = Los[r * kUpdLd + k];
+      }
+    }
   }
 }
 
@@ -396,7 +417,7 @@ hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* su
 
 hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s) {
   if (p.d < 1 || p.d > 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(pooled_update_kernel, dim3(1), dim3(64), 0, s, p);
+  hipLaunchKernelGGL(pooled_update_kernel, dim3(1), dim3(512), 0, s, p);
   return hipGetLastError();
 }
 
