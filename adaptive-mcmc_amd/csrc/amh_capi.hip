@@ -406,6 +406,33 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
   return AMH_OK;
 }
 
+// -------------------------------------------------------------- evaluation --
+int64_t amh_kernel_sum_scratch(int64_t n, int64_t m) { return n > 0 && m > 0 ? amh::kernel_sum_blocks(n, m) : 0; }
+
+int amh_kernel_sum(const float* a, int64_t n, const float* b, int64_t m, int32_t d, float gamma, int32_t skip_diag,
+                   double* scratch, double* out, void* stream) {
+  if (!a || !b || !scratch || !out || n < 1 || m < 1 || d < 1)
+    return fail(nullptr, AMH_EINVAL, "amh_kernel_sum: bad arguments");
+  const hipError_t e = amh::run_kernel_sum(a, n, b, m, d, gamma, skip_diag, scratch, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "amh_kernel_sum");
+  return AMH_OK;
+}
+
+int amh_pairwise_dist2(const float* a, int64_t n, const float* b, int64_t m, int32_t d, float* out, void* stream) {
+  if (!a || !b || !out || n < 1 || m < 1 || d < 1) return fail(nullptr, AMH_EINVAL, "amh_pairwise_dist2: bad arguments");
+  const hipError_t e = amh::run_dist2(a, n, b, m, d, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "amh_pairwise_dist2");
+  return AMH_OK;
+}
+
+int amh_normals(const uint32_t key[2], int64_t n, float* out, void* stream) {
+  if (!key || !out || n < 0) return fail(nullptr, AMH_EINVAL, "amh_normals: bad arguments");
+  if (n == 0) return AMH_OK;
+  const hipError_t e = amh::run_normals(key[0], key[1], n, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "amh_normals");
+  return AMH_OK;
+}
+
 // ------------------------------------------------------- pooled covariance --
 static bool pooled_ok(const amh_pooled_state* s) {
   return s && s->i && s->z && s->potential_energy && s->rng_key && s->mean_accept_prob && s->loc && s->scale &&

@@ -112,6 +112,12 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);
 hipError_t run_asss_step(int model_id, const StepParams& p, hipStream_t s);  // amh_asss.hip
 hipError_t run_asss_pnx(int model_id, const AsssPnxParams& p, hipStream_t s);
+// evaluation metrics (amh_eval.hip)
+int64_t kernel_sum_blocks(int64_t n, int64_t m);
+hipError_t run_kernel_sum(const float* A, int64_t n, const float* B, int64_t m, int d, float gamma, int skip_diag,
+                          double* partials, double* out, hipStream_t s);
+hipError_t run_dist2(const float* A, int64_t n, const float* B, int64_t m, int d, float* out, hipStream_t s);
+hipError_t run_normals(uint32_t k0, uint32_t k1, int64_t n, float* out, hipStream_t s);
 hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s);
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);

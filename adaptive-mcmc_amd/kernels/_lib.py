@@ -25,7 +25,8 @@ AMH_MODEL_DIAMONDS = 4
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",
            "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_asss_step",
-           "amh_asss_sample_pnx")
+           "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
+           "amh_normals")
 
 
 class AmhConfig(ctypes.Structure):
@@ -82,6 +83,14 @@ def lib():
     L.amh_asss_step.restype = ctypes.c_int
     L.amh_asss_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, I32, P, P]
     L.amh_asss_sample_pnx.restype = ctypes.c_int
+    L.amh_kernel_sum_scratch.argtypes = [I64, I64]
+    L.amh_kernel_sum_scratch.restype = I64
+    L.amh_kernel_sum.argtypes = [P, I64, P, I64, I32, F, I32, P, P, P]
+    L.amh_kernel_sum.restype = ctypes.c_int
+    L.amh_pairwise_dist2.argtypes = [P, I64, P, I64, I32, P, P]
+    L.amh_pairwise_dist2.restype = ctypes.c_int
+    L.amh_normals.argtypes = [ctypes.POINTER(ctypes.c_uint32), I64, P, P]
+    L.amh_normals.restype = ctypes.c_int
     for name in EXPORTS[:10]:
         getattr(L, name).restype = ctypes.c_int if name != "amh_last_error" else ctypes.c_char_p
     _lib = L

@@ -1,0 +1,152 @@
+"""Sample-quality metrics of the reference (python/utils/evaluation.py) on the
+GPU, same function names and arguments.
+
+  pth_moment_rmse          evaluation.py:13-40    column means of x^p (device)
+  wasserstein_dist11_p     evaluation.py:43-67    optimal 1-1 coupling; the
+                                                   reference runs scipy's
+                                                   Hungarian on the host, and
+                                                   so does this one
+  wasserstein_1d           evaluation.py:139-162  sorted differences (device)
+  max_sliced_wasserstein   evaluation.py:165-206  projections = one GEMM
+                                                   (hipBLASLt through torch),
+                                                   per-direction sorts
+  gaussian_kernel          evaluation.py:209-230  exp(-gamma D2), D2 from the
+                                                   HIP pairwise-distance kernel
+  mmd2_unbiased            evaluation.py:233-266  three HIP Gaussian-kernel
+                                                   sums (amh_kernel_sum,
+                                                   diagonal skipped in-kernel)
+  mmd_heuristic            evaluation.py:269-294  median bandwidth from the
+                                                   HIP distance matrix
+
+wasserstein_sinkhorn(_unbiased) (evaluation.py:70-136) call the `ott` OT
+solver library, which is not available here; they are not provided.
+
+Inputs may be numpy arrays or torch tensors; they are moved to the current
+CUDA device as float32.  Directions for max_sliced_wasserstein come from the
+build's Philox stream (the reference uses jax.random.normal), so values agree
+with the reference in distribution, not bit for bit.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from kernels import _lib
+from kernels.random import as_key
+
+__all__ = ["pth_moment_rmse", "wasserstein_dist11_p", "wasserstein_1d", "max_sliced_wasserstein", "gaussian_kernel",
+           "mmd2_unbiased", "mmd_heuristic"]
+
+
+def _dev(x) -> torch.Tensor:
+    if isinstance(x, torch.Tensor):
+        t = x.detach()
+    else:
+        t = torch.as_tensor(np.asarray(x))
+    dev = t.device if t.is_cuda else torch.device("cuda", torch.cuda.current_device())
+    return t.to(device=dev, dtype=torch.float32).contiguous()
+
+
+def _stream(t: torch.Tensor):
+    return _lib.stream_ptr(t.device.index)
+
+
+def _kernel_sum(a: torch.Tensor, b: torch.Tensor, gamma: float, skip_diag: bool) -> float:
+    L = _lib.lib()
+    n, d = a.shape
+    m = b.shape[0]
+    scratch = torch.empty(max(1, int(L.amh_kernel_sum_scratch(n, m))), dtype=torch.float64, device=a.device)
+    out = torch.empty(1, dtype=torch.float64, device=a.device)
+    with torch.cuda.device(a.device.index):
+        _lib.check(L.amh_kernel_sum(_lib.ptr(a), n, _lib.ptr(b), m, d, float(gamma), int(bool(skip_diag)),
+                                    _lib.ptr(scratch), _lib.ptr(out), _stream(a)))
+    return float(out.item())
+
+
+def _dist2(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    L = _lib.lib()
+    n, d = a.shape
+    m = b.shape[0]
+    out = torch.empty(n, m, dtype=torch.float32, device=a.device)
+    with torch.cuda.device(a.device.index):
+        _lib.check(L.amh_pairwise_dist2(_lib.ptr(a), n, _lib.ptr(b), m, d, _lib.ptr(out), _stream(a)))
+    return out
+
+
+def pth_moment_rmse(x, y, p=2.0) -> float:
+    """||mean(x^p) - mean(y^p)||_2 over columns (evaluation.py:13-40)."""
+    x, y = _dev(x), _dev(y)
+    return float(torch.linalg.vector_norm(torch.mean(x ** p, dim=0) - torch.mean(y ** p, dim=0)))
+
+
+def wasserstein_dist11_p(u_values, v_values, ord=2.0) -> float:
+    """Optimal 1-1 coupling cost (evaluation.py:43-67; host, as the reference)."""
+    from scipy.optimize import linear_sum_assignment
+    from scipy.spatial import distance_matrix
+    u = np.asarray(u_values.cpu() if hasattr(u_values, "cpu") else u_values)
+    v = np.asarray(v_values.cpu() if hasattr(v_values, "cpu") else v_values)
+    cost = distance_matrix(u, v, p=ord)
+    r, c = linear_sum_assignment(cost)
+    return float(cost[r, c].mean())
+
+
+def wasserstein_1d(mu, nu, p=1.0):
+    """mean(|sort(mu) - sort(nu)|^p)^(1/p) along the last axis (evaluation.py:139-162)."""
+    mu, nu = _dev(mu), _dev(nu)
+    diff = torch.abs(torch.sort(mu, dim=-1).values - torch.sort(nu, dim=-1).values)
+    return torch.mean(diff ** p, dim=-1) ** (1.0 / p)
+
+
+def _directions(rng_key, n_directions: int, d: int, device) -> torch.Tensor:
+    """n_directions unit vectors: normals of the build's Philox stream
+    (amh_normals), each row normalised (evaluation.py:189-190)."""
+    z = torch.empty(n_directions, d, dtype=torch.float32, device=device)
+    with torch.cuda.device(device.index):
+        _lib.check(_lib.lib().amh_normals(_lib.key_arr(as_key(rng_key)), n_directions * d, _lib.ptr(z),
+                                          _lib.stream_ptr(device.index)))
+    return z / torch.linalg.norm(z, dim=1, keepdim=True)
+
+
+def max_sliced_wasserstein(mu, nu, rng_key, p=1.0, n_directions=1000) -> float:
+    """max over random unit directions of the 1-D Wasserstein-p distance of the
+    projections (evaluation.py:165-206)."""
+    mu, nu = _dev(mu), _dev(nu)
+    dirs = _directions(rng_key, int(n_directions), mu.shape[1], mu.device)
+    pm = (mu @ dirs.T).T.contiguous()  # [n_dir, n]
+    pn = (nu @ dirs.T).T.contiguous()
+    return float(torch.max(wasserstein_1d(pm, pn, p=p)))
+
+
+def gaussian_kernel(x, y, gamma):
+    """exp(-gamma ||x_i - y_j||^2) as an [n, m] device matrix (evaluation.py:209-230)."""
+    x, y = _dev(x), _dev(y)
+    return torch.exp(-float(gamma) * _dist2(x, y))
+
+
+def mmd2_unbiased(x, y, gamma=1.0) -> float:
+    """Unbiased MMD^2 with a Gaussian kernel (evaluation.py:233-266)."""
+    x, y = _dev(x), _dev(y)
+    n, m = x.shape[0], y.shape[0]
+    sxx = _kernel_sum(x, x, gamma, True)
+    syy = _kernel_sum(y, y, gamma, True)
+    sxy = _kernel_sum(x, y, gamma, False)
+    return sxx / (n * (n - 1)) + syy / (m * (m - 1)) - 2.0 * sxy / (n * m)
+
+
+def mmd_heuristic(x, y) -> float:
+    """Biased MMD with the median heuristic bandwidth gamma = 4 / median of the
+    reference sample's squared distances (evaluation.py:269-294)."""
+    x, y = _dev(x), _dev(y)
+    n, m = x.shape[0], y.shape[0]
+    d2 = _dist2(y, y).reshape(-1)
+    k = d2.numel()
+    lo = torch.kthvalue(d2, (k + 1) // 2).values
+    hi = torch.kthvalue(d2, k // 2 + 1).values
+    med = float(0.5 * (lo.double() + hi.double())) if k % 2 == 0 else float(lo)
+    gamma = 4.0 / med
+    sxx = _kernel_sum(x, x, gamma, False)
+    syy = _kernel_sum(y, y, gamma, False)
+    sxy = _kernel_sum(x, y, gamma, False)
+    return math.sqrt(max(sxx / n ** 2 + syy / m ** 2 - 2.0 * sxy / (n * m), 0.0))

@@ -150,6 +150,23 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
                         int64_t n_samples, const float* loc, const float* scale_packed, int32_t n,
                         float* out, void* stream);
 
+/* ----------------------------------------------------------- evaluation ----
+ * python/utils/evaluation.py:223-294 (gaussian_kernel / mmd2_unbiased /
+ * mmd_heuristic).  No handle: work goes to `stream` on the current device.
+ * amh_kernel_sum: *out (device double) = sum over i < n, j < m of
+ * exp(-gamma ||a_i - b_j||^2), pairs i == j skipped if skip_diag; a [n][d],
+ * b [m][d] device float; scratch: amh_kernel_sum_scratch(n, m) device
+ * doubles.  Deterministic (fixed-order reduction). */
+int64_t amh_kernel_sum_scratch(int64_t n, int64_t m);
+int amh_kernel_sum(const float* a, int64_t n, const float* b, int64_t m, int32_t d, float gamma,
+                   int32_t skip_diag, double* scratch, double* out, void* stream);
+/* out[i] = standard normal i of the stream keyed by key[2] (host memory),
+ * for the random directions of max_sliced_wasserstein (evaluation.py:189). */
+int amh_normals(const uint32_t key[2], int64_t n, float* out, void* stream);
+/* out [n][m] = ||a_i - b_j||^2 (the median bandwidth heuristic, evaluation.py:286). */
+int amh_pairwise_dist2(const float* a, int64_t n, const float* b, int64_t m, int32_t d, float* out,
+                       void* stream);
+
 /* ---------------------------------------------------- pooled covariance ----
  * Regime B (build-defined, no reference analogue): every chain
  * proposes with ONE shared adapt state, and the adaptation of arwmh.py:180-197

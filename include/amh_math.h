@@ -78,6 +78,7 @@ AMH_HD amh_u32x4 amh_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32
 #define AMH_TAG_INIT     0x54494E49u /* init_to_uniform draws                 */
 #define AMH_TAG_STEP     0x50455453u /* per-step proposal / accept draws      */
 #define AMH_TAG_SPLIT    0x54494C50u /* key splitting (sample_Pnx keys)       */
+#define AMH_TAG_EVAL     0x4C415645u /* evaluation draws (sliced directions) */
 #define AMH_TAG_ASSS     0x53535341u /* ASSS per-step draws (c2 = 0: v, u_t,
                                         theta_0; c2 = 1: shrink uniforms)   */
 

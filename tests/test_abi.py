@@ -14,7 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def header_symbols():
     src = open(os.path.join(ROOT, "include", "amh.h")).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"^\s*(?:int|const char\s*\*)\s*(amh_\w+)\s*\(", src, flags=re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int64_t|int|const char\s*\*)\s*(amh_\w+)\s*\(", src, flags=re.M)))
 
 
 @pytest.fixture(scope="module")
