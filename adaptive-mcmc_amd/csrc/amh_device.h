@@ -205,6 +205,7 @@ __device__ __forceinline__ int64_t col_off(int d, int j) {
 // completed by lds_wait(), which ties the loaded values so no use can be
 // scheduled before the wait.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(3))) const float lds_cfloat;
 __device__ __forceinline__ uint32_t lds_addr(const float* p) {
   return (uint32_t)(uintptr_t)(lds_cfloat*)p;
@@ -271,8 +272,13 @@ struct GaussianM {
     const float diff = act ? x - c.mr : 0.0f;
     const uint32_t prow = lds_addr(lds + (act ? r : 0) * ld(d));
     // partial sums over columns j mod 4 (four independent FMA chains); the
-    // row is read 16 columns at a time (four ds_read_b128 then one wait)
+    // row is read 16 columns at a time (four ds_read_b128 then one wait).
+    // Columns (j, j+1) go through one v_pk_fma_f32 into the accumulator pair
+    // (j mod 4, j+1 mod 4): each half is the same fmaf.  A column past d
+    // pairs a zero (padded row) with a zero (inactive lane's diff) and
+    // leaves its accumulator unchanged.
     float y4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
     static_for<(G + 15) / 16>([&](auto B) {
       constexpr int b = B;
       if (16 * b < d) {
@@ -282,15 +288,35 @@ struct GaussianM {
           pv[Q] = (4 * (4 * b + Q) < d) ? lds_ld4<16 * (4 * b + Q)>(prow) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
         });
         lds_wait(pv[0], pv[1], pv[2], pv[3]);
-        static_for<16>([&](auto K) {
-          constexpr int j = 16 * b + K;
-          if constexpr (j < G) {
-            if (j < d) y4[K & 3] = fmaf(act ? pv[K / 4][K % 4] : 0.0f, Grp<G>::template bcast<j>(diff), y4[K & 3]);
-          }
-        });
+        if constexpr (G == 1) {
+          y4[0] = fmaf(act ? pv[0][0] : 0.0f, diff, y4[0]);
+        } else {
+          static_for<8>([&](auto K2) {
+            constexpr int j = 16 * b + 2 * K2;
+            if constexpr (j < G) {
+              if (j < d) {
+                const f32x4 q = pv[K2 / 2];
+                const f32x2v pp = (K2 % 2 == 0) ? f32x2v{q[0], q[1]} : f32x2v{q[2], q[3]};
+                const f32x2v pa = act ? pp : f32x2v{0.0f, 0.0f};
+                const f32x2v bp = {Grp<G>::template bcast<j>(diff), Grp<G>::template bcast<j + 1>(diff)};
+                if constexpr (K2 % 2 == 0) {
+                  y01 = __builtin_elementwise_fma(pa, bp, y01);
+                } else {
+                  y23 = __builtin_elementwise_fma(pa, bp, y23);
+                }
+              }
+            }
+          });
+        }
         __builtin_amdgcn_sched_barrier(0);
       }
     });
+    if constexpr (G > 1) {
+      y4[0] = y01[0];
+      y4[1] = y01[1];
+      y4[2] = y23[0];
+      y4[3] = y23[1];
+    }
     const float y = (y4[0] + y4[1]) + (y4[2] + y4[3]);
     const float q = act ? diff * y : 0.0f;
     const float S = Grp<G>::sum(q);
