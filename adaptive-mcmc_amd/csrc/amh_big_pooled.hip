@@ -119,10 +119,15 @@ __global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsPara
 }
 
 // ------------------------------------------------------------------- stats --
-// 8 waves; 36 (at d = 256) lower tile pairs (I >= J) of S_dd, wave w owns
-// pairs w, w + 8, ...; the chunk's chains feed the MFMA K dimension in order.
+// 8 waves per block; a chunk's lower tile pairs (I >= J) of S_dd (36 at d =
+// 256) are split over `split` blocks (blockIdx.y) so that a run of few chunks
+// still fills the chip: block part q owns pairs [q * per, (q + 1) * per) and
+// wave w of it local pairs w, w + 8, ...  Every part recomputes the chunk's
+// accept flags and deltas (cheap); part 0 alone writes z', U', S_d, S_a and the
+// count.  The chunk's chains feed the MFMA K dimension in order, so the split
+// does not change any sum.
 __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams p, const float* xprop,
-                                                               const float* pep) {
+                                                               const float* pep, int per) {
   extern __shared__ float lds[];
   const int d = p.d;
   const int nt = d / 32;
@@ -138,18 +143,25 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
   const int h = lane >> 5, i = lane & 31;
   const int32_t it = p.i[0];
   const int64_t base = (int64_t)blockIdx.x * kBigChunk;
+  const int part = blockIdx.y;
+  const bool writer = part == 0;
+  const int pair0 = part * per;
+  const int pair1 = (pair0 + per < npairs) ? pair0 + per : npairs;
   float sd = 0.0f, sa = 0.0f;
   int64_t cnt = 0;
   f32x16 acc[5];
   int pI[5], pJ[5];
+  bool own[5];
   static_for<5>([&](auto S) {
     acc[S] = f32x16{};
-    const int pp = w + 8 * S;
+    const int pp = pair0 + w + 8 * S;
+    own[S] = pp < pair1;
     int I = 0;
     while ((I + 1) * (I + 2) / 2 <= pp) ++I;
     pI[S] = I;
     pJ[S] = pp - I * (I + 1) / 2;
   });
+  const int kk2 = tid & 255, half = tid >> 8;  // gather: two chains per pass, k = tid mod 256
   for (int t = 0; t < kBigChunk / 64; ++t) {
     const int64_t c0 = base + 64 * t;
     const int64_t left = p.C - c0;
@@ -168,33 +180,39 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
         const float ex = amh_expf(pe - pp);
         a = (ex > 1.0f) ? 1.0f : ex;
         acc_f = u < a;
-        p.pe_out[c] = acc_f ? pp : pe;
+        if (writer) p.pe_out[c] = acc_f ? pp : pe;
       }
       flag[tid] = acc_f;
       alph[tid] = a;
     }
     __syncthreads();
-    for (int idx = tid; idx < 64 * d; idx += 512) {
-      const int cc = idx / d, k = idx - cc * d;
-      float dv = 0.0f;
-      if (cc < nv) {
-        const int64_t c = c0 + cc;
-        const float zn = flag[cc] ? xprop[c * d + k] : p.z[c * d + k];
-        p.z_out[c * d + k] = zn;
-        dv = zn - p.mu[k];
+    if (kk2 < d) {
+      const float muk = p.mu[kk2];
+      for (int cp = 0; cp < 32; ++cp) {
+        const int cc = 2 * cp + half;
+        float dv = 0.0f;
+        if (cc < nv) {
+          const int64_t c = c0 + cc;
+          const float* src = flag[cc] ? xprop : p.z;
+          const float zn = src[c * d + kk2];
+          if (writer) p.z_out[c * d + kk2] = zn;
+          dv = zn - muk;
+        }
+        Dl[kk2 * kLd + cc] = dv;
       }
-      Dl[k * kLd + cc] = dv;
     }
     __syncthreads();
-    if (tid < d) {
-      for (int c = 0; c < nv; ++c) sd = sd + Dl[tid * kLd + c];
-    }
-    if (tid == 511) {
-      for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+    if (writer) {
+      if (tid < d) {
+        for (int c = 0; c < nv; ++c) sd = sd + Dl[tid * kLd + c];
+      }
+      if (tid == 511) {
+        for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+      }
     }
     cnt += nv;
     static_for<5>([&](auto S) {
-      if (w + 8 * S < npairs) {
+      if (own[S]) {
         const int ra = (32 * pI[S] + i) * kLd, rb = (32 * pJ[S] + i) * kLd;
         int kk = 0;
         for (; kk + 16 <= nv; kk += 16) {
@@ -213,13 +231,15 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
     __syncthreads();
   }
   double* out = p.partials + (int64_t)blockIdx.x * V;
-  if (tid < d) out[tid] = (double)sd;
-  if (tid == 511) {
-    out[d + P] = (double)sa;
-    out[d + P + 1] = (double)cnt;
+  if (writer) {
+    if (tid < d) out[tid] = (double)sd;
+    if (tid == 511) {
+      out[d + P] = (double)sa;
+      out[d + P + 1] = (double)cnt;
+    }
   }
   static_for<5>([&](auto S) {
-    if (w + 8 * S < npairs) {
+    if (own[S]) {
       static_for<16>([&](auto R) {
         const int row = 32 * pI[S] + (R & 3) + 8 * (R >> 2) + 4 * h;
         const int col = 32 * pJ[S] + i;
@@ -326,12 +346,21 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
       float a[32];
       static_for<32>([&](auto K) { a[K] = (K <= ii) ? A[a4_base(d, p0 + K) + r] : 0.0f; });
       bool ok = true;
+      // the next pivot is formed from lane k+1's own two values (readlane),
+      // the same fmaf its rank-one update applies, so the pivot chain does
+      // not wait for the LDS round trip of the column
+      float piv = rdlane(a[0], 0);
       static_for<32>([&](auto K) {
         constexpr int k = K;
-        const float piv = rdlane(a[k], k);
         ok = ok && (piv > 0.0f) && amh_isfinite(piv);
         const float ljj = sqrtf(piv);
         a[k] = a[k] / ljj;
+        float l1 = 0.0f;  // L_{k+1,k}: column k+1's update and the next pivot skip the LDS round trip
+        if constexpr (k + 1 < 32) {
+          l1 = rdlane(a[k], k + 1);
+          piv = fmaf(-l1, l1, rdlane(a[k + 1], k + 1));
+          a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
+        }
         Lt[k * 32 + ii] = a[k];
         Lt[k * 32 + k] = ljj;  // uniform store, after the lane stores
         if constexpr (k + 1 < 32) {
@@ -340,7 +369,7 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
             const f32x4 v = *(const f32x4*)&Lt[k * 32 + m0];
             static_for<4>([&](auto E) {
               constexpr int m = m0 + E;
-              if constexpr (m > k) a[m] = fmaf(-a[k], v[(int)E], a[m]);
+              if constexpr (m > k + 1) a[m] = fmaf(-a[k], v[(int)E], a[m]);
             });
           });
         }
@@ -392,8 +421,8 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
         const int cbase = a4_base(d, c0 + Y) + r0;
         static_for<8>([&](auto X) { t[X][(int)Y / 2][(int)Y % 2] = A[cbase + X]; });
       });
+      int cb = a4_base(d, p0);
       for (int j = 0; j < 32; ++j) {
-        const int cb = a4_base(d, p0 + j);
         const f32x4 r4a = *(const f32x4*)&A[cb + r0], r4b = *(const f32x4*)&A[cb + r0 + 4];
         const f32x4 c4a = *(const f32x4*)&A[cb + c0], c4b = *(const f32x4*)&A[cb + c0 + 4];
         const float lr[8] = {r4a[0], r4a[1], r4a[2], r4a[3], r4b[0], r4b[1], r4b[2], r4b[3]};
@@ -403,6 +432,7 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
           const f32x2 nl = f32x2{-lr[X], -lr[X]};
           static_for<4>([&](auto Y) { t[X][Y] = __builtin_elementwise_fma(nl, lc[Y], t[X][Y]); });
         });
+        cb += d - ((p0 + j + 1) & ~3);  // a4_base(d, p0 + j + 1)
       }
       static_for<8>([&](auto Y) {
         const int c = c0 + Y;
@@ -492,8 +522,16 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
   e = run_big_potential(q, s);
   if (e != hipSuccess) return e;
   const int64_t nch = pooled_big_chunks(p.C);
-  hipLaunchKernelGGL(pooled_big_stats_kernel, dim3((unsigned)nch), dim3(512),
-                     ((size_t)d * kLd + 128) * sizeof(float), s, p, (const float*)xprop, (const float*)pep);
+  // split each chunk's tile pairs over enough blocks to cover the CUs
+  const int nt = d / 32, npairs = nt * (nt + 1) / 2;
+  int split = (int)((256 + nch - 1) / nch);
+  const int max_split = (npairs + 7) / 8;  // at least 8 pairs (one per wave) per part
+  if (split > max_split) split = max_split;
+  if (split < 1) split = 1;
+  const int per = (npairs + split - 1) / split;
+  split = (npairs + per - 1) / per;
+  hipLaunchKernelGGL(pooled_big_stats_kernel, dim3((unsigned)nch, (unsigned)split), dim3(512),
+                     ((size_t)d * kLd + 128) * sizeof(float), s, p, (const float*)xprop, (const float*)pep, per);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   return pooled_reduce(p.partials, nch, V, sums, s);
