@@ -123,6 +123,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
     ap.add_argument("--no-pooled", action="store_true")
+    ap.add_argument("--no-fused", action="store_true", help="skip the fused 50-step launch (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -178,12 +179,14 @@ def main():
     achieved_gbs = per_launch_bytes / (kern_ms * 1e-3) / 1e9
 
     # fused multi-step launch (numpyro fori_collect semantics, state on chip)
-    fused_steps = 50
-    torch.cuda.synchronize()
-    f0 = time.perf_counter()
-    k.sample_(st, fused_steps)
-    torch.cuda.synchronize()
-    fused_rate = C * fused_steps / (time.perf_counter() - f0)
+    fused_rate = None
+    if not args.no_fused:
+        fused_steps = 50
+        torch.cuda.synchronize()
+        f0 = time.perf_counter()
+        k.sample_(st, fused_steps)
+        torch.cuda.synchronize()
+        fused_rate = C * fused_steps / (time.perf_counter() - f0)
 
     ess = None
     if not args.no_ess and rank == 0:
@@ -238,7 +241,7 @@ def main():
                          "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
             "cpu_baseline": cpu,
             "ess": ess,
-            "fused_chain_steps_per_s": fused_rate * world,
+            "fused_chain_steps_per_s": fused_rate * world if fused_rate else None,
             "pooled": pooled,
         }
         print(json.dumps(line))
