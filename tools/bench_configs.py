@@ -56,7 +56,7 @@ def run_regime_a(name, kernel, C, d, kwargs, steps, warmup, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64,asss64,asss_es")
+    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64,asss64,asss_es,pnx")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
@@ -89,6 +89,28 @@ def main():
         k = ASSS(model=P.eight_schools, num_chains=C, device=dev)
         print(json.dumps(run_regime_a("ASSS eight schools", k, C, 10, dict(P.EIGHT_SCHOOLS_DATA), args.steps,
                                       args.warmup, dev)), flush=True)
+    if "pnx" in want:
+        # many-chain frozen kernel (sample_Pnx, the Lipschitz sweeps' sampler):
+        # 5e4 start points x 1e3 chains each x 1 step, eight schools
+        data = dict(P.EIGHT_SCHOOLS_DATA)
+        for K in (ARWMH, ASSS):
+            k = K(model=P.eight_schools, num_chains=64, device=dev)
+            st = k.init(PRNGKey(0), 0, None, (), data)
+            k.sample_(st, 2000)
+            x = st.z[:50].repeat(1000, 1).contiguous()  # 5e4 points
+            adapt = st.adapt_state
+            shared = (adapt.loc[0], adapt.scale[0]) + ((adapt.log_step_size[0],) if K is ARWMH else ())
+            k.sample_Pnx(PRNGKey(1), x, shared, n=1, n_samples=1000)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps = 5
+            for r in range(reps):
+                k.sample_Pnx(PRNGKey(2 + r), x, shared, n=1, n_samples=1000)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            print(json.dumps({"config": f"{K.__name__}.sample_Pnx eight schools", "chains": 50000 * 1000, "dim": 10,
+                              "steps": 1, "value": reps * 5e7 / wall, "unit": "chain-steps/s",
+                              "ms_per_call": wall / reps * 1e3}), flush=True)
     for key, d, C, kappa in (("gauss256_pooled", 256, 32768, 4.0), ("pooled64", 64, 65536, 2.0)):
         if key not in want:
             continue
