@@ -25,7 +25,7 @@ namespace {
 // partial sums over j mod 4, read 16 columns at a time.
 __device__ __forceinline__ float lds_row_dot64(uint32_t prow, int d, float v, bool act) {
   using Gp = Grp<64>;
-  float y4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+  f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
   static_for<4>([&](auto B) {
     constexpr int b = B;
     if (16 * b < d) {
@@ -34,14 +34,26 @@ __device__ __forceinline__ float lds_row_dot64(uint32_t prow, int d, float v, bo
         pv[Q] = (4 * (4 * b + Q) < d) ? lds_ld4<16 * (4 * b + Q)>(prow) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
       });
       lds_wait(pv[0], pv[1], pv[2], pv[3]);
-      static_for<16>([&](auto K) {
-        constexpr int j = 16 * b + K;
-        if (j < d) y4[K & 3] = fmaf(act ? pv[K / 4][K % 4] : 0.0f, Gp::template bcast<j>(v), y4[K & 3]);
+      // columns (j, j+1) through one v_pk_fma_f32 into accumulators (j mod 4,
+      // j+1 mod 4); a column past d adds 0 * 0 (padded row, inactive lane)
+      static_for<8>([&](auto K2) {
+        constexpr int j = 16 * b + 2 * K2;
+        if (j < d) {
+          const f32x4 q = pv[K2 / 2];
+          const f32x2v pp = (K2 % 2 == 0) ? f32x2v{q[0], q[1]} : f32x2v{q[2], q[3]};
+          const f32x2v pa = act ? pp : f32x2v{0.0f, 0.0f};
+          const f32x2v bp = {Gp::template bcast<j>(v), Gp::template bcast<j + 1>(v)};
+          if constexpr (K2 % 2 == 0) {
+            y01 = __builtin_elementwise_fma(pa, bp, y01);
+          } else {
+            y23 = __builtin_elementwise_fma(pa, bp, y23);
+          }
+        }
       });
       __builtin_amdgcn_sched_barrier(0);
     }
   });
-  return (y4[0] + y4[1]) + (y4[2] + y4[3]);
+  return (y01[0] + y01[1]) + (y23[0] + y23[1]);
 }
 
 __host__ __device__ inline int pooled_ld(int d) { return ((d + 3) & ~3) + 4; }
@@ -135,10 +147,17 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
     // pooled statistics (float32 over this wave's chains, in chain order)
     const float delta = act ? zn - mu : 0.0f;
     sd = sd + delta;
-    static_for<64>([&](auto K) {
-      constexpr int k = K;
-      if (k < d) S[k] = fmaf(delta, Gp::template bcast<k>(delta), S[k]);
-      column_fence<k>();
+    // (S_k, S_k+1) += delta_r (delta_k, delta_k+1): one v_pk_fma_f32 per pair
+    // (each half is the same fmaf; past d the broadcast delta is 0)
+    static_for<32>([&](auto K2) {
+      constexpr int k = 2 * K2;
+      if (k < d) {
+        const f32x2v bp = {Gp::template bcast<k>(delta), Gp::template bcast<k + 1>(delta)};
+        const f32x2v sp = __builtin_elementwise_fma(f32x2v{delta, delta}, bp, f32x2v{S[k], S[k + 1]});
+        S[k] = sp[0];
+        S[k + 1] = sp[1];
+      }
+      column_fence<k + 1>();
     });
     sa = sa + alpha;
   }
