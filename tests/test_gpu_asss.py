@@ -114,3 +114,15 @@ def test_asss_eight_schools_posterior(gpu):
     # notebook min U 41.17 over 1e4 draws; the minimum over 2.56M draws sits lower
     assert 39.5 < float(m.get_extra_fields()["potential_energy"].min()) < 41.5
     assert "Iteration: 275000" in k.get_diagnostics_str(m.last_state)
+
+
+@pytest.mark.parametrize("d,C", [(1, 1), (1, 65), (2, 3), (3, 1), (64, 1)])
+def test_asss_edge_sizes(d, C, gpu, orc):
+    """Group widths 1..64 at tiny chain counts (ragged last wave, one chain)."""
+    k, st, om, ost = _init("gaussian", C, orc, d=d, num_warmup=3)
+    for n in (1, 5):
+        st, cz, _ = k.run(st, n, thinning=1, collect_z=True)
+        ocz, _ = orc.asss_step(om, ost, n, num_warmup=3, collect_z=True)
+        torch.cuda.synchronize()
+        assert_bitequal(st, ost, f"d={d} C={C} n={n}")
+        np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), ocz.view(np.uint32))
