@@ -519,6 +519,12 @@ __device__ __forceinline__ float lookup_gamma(const StepParams& p, int32_t n) {
 // that must not touch memory get an out-of-range voffset (loads return 0,
 // stores are dropped by the hardware range check).
 constexpr uint32_t kOOB = 0x80000000u;
+#ifndef AMH_STORE_AUX
+#define AMH_STORE_AUX 2  // cache policy of state stores: nt (streaming, written once per launch)
+#endif
+#ifndef AMH_LOAD_AUX
+#define AMH_LOAD_AUX 2  // cache policy of the factor's DMA loads: nt (read once per launch)
+#endif
 
 struct Buf {
   __amdgpu_buffer_rsrc_t rs;
@@ -529,7 +535,7 @@ struct Buf {
     return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, (int)voff, (int)soff, 0));
   }
   __device__ __forceinline__ void st(float v, uint32_t voff, uint32_t soff) const {
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, (int)voff, (int)soff, AMH_STORE_AUX);
   }
 };
 

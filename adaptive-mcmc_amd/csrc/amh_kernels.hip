@@ -54,10 +54,10 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
     // DMA inside this wave's buffer (an LDS-DMA writes base + 4*size*lane)
     const uint32_t n16 = vec ? (total / 1024u) * 1024u : 0u;
     for (uint32_t o = 0; o < n16; o += 1024u)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 16, (int)(o + 16u * lane), 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 16, (int)(o + 16u * lane), 0, 0, AMH_LOAD_AUX);
     for (uint32_t o = n16; o < total; o += 256u) {
       if (o + 4u * lane < total)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 4, (int)(o + 4u * lane), 0, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(b.rs, to_lds(wL + o / 4u), 4, (int)(o + 4u * lane), 0, 0, AMH_LOAD_AUX);
     }
   }
   {
