@@ -219,7 +219,7 @@ __device__ __forceinline__ void asss_transition(const StepParams& p, float (&U)[
 }
 
 template <int DMAX, template <int> class M, bool EXACT>
-__global__ __launch_bounds__(kBlock) void asss_step_kernel(StepParams p) {
+__global__ __launch_bounds__(kBlock, (EXACT && DMAX == 64) ? 4 : 1) void asss_step_kernel(StepParams p) {
   constexpr int G = DMAX;
   using Gp = Grp<G>;
   extern __shared__ float lds[];
