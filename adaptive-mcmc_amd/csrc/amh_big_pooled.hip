@@ -310,26 +310,13 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
   const float abar = (float)(sums[d + P] / N);
   const float maccn = macc + (abar - macc) / (float)n;
   const float lamn = lam + gamma * (abar - p.target);
-  const double g = (double)gamma;
-  // (0) A = float((1-g) Sigma + g S_dd / N): wave w takes columns w, w + 16,
-  // ...; a column's loads are all issued before its LDS stores
-  for (int j = w; j < d; j += 16) {
-    const int64_t co = col_off(d, j);
-    const int len = d - j, ab = a4_base(d, j);
-    double cv[4], sv[4];
-    static_for<4>([&](auto Q) {
-      const int rr = 64 * Q + lane;
-      cv[Q] = rr < len ? p.in.cov[co + rr] : 0.0;
-      sv[Q] = rr < len ? sums[d + co + rr] : 0.0;
-    });
-    static_for<4>([&](auto Q) {
-      const int rr = 64 * Q + lane;
-      if (rr < len) {
-        const double a = (1.0 - g) * cv[Q];
-        const double b = g * (sv[Q] / N);
-        A[ab + j + rr] = (float)(a + b);
-      }
-    });
+  // (0) A = float((1-g) Sigma + g S_dd / N), formed in the 4-row-aligned
+  // layout by pooled_big_prep_kernel (all CUs): one coalesced 16-B copy
+  {
+    const int nA = d * (d + 4) / 2;
+    const f32x4* src = (const f32x4*)p.scratch;
+    f32x4* dst = (f32x4*)A;
+    for (int q = tid; q < nA / 4; q += 1024) dst[q] = src[q];
   }
   if (tid == 0) okv = 1;
   __syncthreads();
@@ -447,32 +434,33 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
   }
   const bool ok = okv != 0;
   const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
-  // (4) write-out, column-wise (coalesced); each element's as_change term
-  // replaces it in LDS (in-place safe: the old factor is read before the new
-  // one is written)
+  // (4) the new factor back to the staging buffer (coalesced; the copy to
+  // out.scale and out.cov is pooled_big_post_kernel's, on all CUs) with the
+  // ok flag and gamma; then each element's as_change term replaces it in LDS
+  // (old factor read column-wise from HBM) and is summed by rows
+  {
+    const int nA = d * (d + 4) / 2;
+    f32x4* dst = (f32x4*)p.scratch;
+    const f32x4* src = (const f32x4*)A;
+    for (int q = tid; q < nA / 4; q += 1024) dst[q] = src[q];
+    if (tid == 0) {
+      ((int*)p.scratch)[nA] = ok ? 1 : 0;
+      p.scratch[nA + 1] = gamma;
+    }
+  }
+  __syncthreads();
   for (int j = w; j < d; j += 16) {
     const int64_t co = col_off(d, j);
     const int len = d - j, ab = a4_base(d, j);
     float lo[4];
-    double cv[4], sv[4];
     static_for<4>([&](auto Q) {
       const int rr = 64 * Q + lane;
       lo[Q] = rr < len ? p.in.scale[co + rr] : 0.0f;
-      cv[Q] = rr < len ? p.in.cov[co + rr] : 0.0;
-      sv[Q] = (ok && rr < len) ? sums[d + co + rr] : 0.0;
     });
     static_for<4>([&](auto Q) {
       const int rr = 64 * Q + lane;
       if (rr < len) {
         const float ln = ok ? A[ab + j + rr] : lo[Q];
-        if (ok) {
-          const double a = (1.0 - g) * cv[Q];
-          const double b = g * (sv[Q] / N);
-          p.out.cov[co + rr] = a + b;
-        } else {
-          p.out.cov[co + rr] = cv[Q];
-        }
-        p.out.scale[co + rr] = ln;
         A[ab + j + rr] = (ln * e1) - (lo[Q] * e0);
       }
     });
@@ -504,6 +492,52 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
   if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
   US(6)
   US_FLUSH
+}
+
+// Sigma' = (1-g) Sigma + g S_dd / N rounded to float, in the update's
+// 4-row-aligned layout (block k = column k; all CUs)
+__global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams p) {
+  const int d = p.d;
+  const int k = blockIdx.x;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const double N = p.sums[d + P + 1];
+  const int32_t it = p.in.i[0];
+  const int32_t n = (it < p.W) ? it + 1 : it + 1 - p.W;
+  const double g = (double)amh_lr_gamma(n, p.a);
+  const int64_t co = col_off(d, k);
+  const int ab = a4_base(d, k);
+  for (int rr = threadIdx.x; rr < d - k; rr += 256) {
+    const double a = (1.0 - g) * p.in.cov[co + rr];
+    const double b = g * (p.sums[d + co + rr] / N);
+    p.scratch[ab + k + rr] = (float)(a + b);
+  }
+}
+
+// out.scale = the new factor (or the kept one), out.cov = Sigma' (or the kept
+// one); element-wise, in-place safe (block k = column k; all CUs)
+__global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams p) {
+  const int d = p.d;
+  const int k = blockIdx.x;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  // ok flag and gamma from the update kernel (p.in.i may alias p.out.i, which
+  // the update kernel has already advanced)
+  const bool ok = ((const int*)p.scratch)[d * (d + 4) / 2] != 0;
+  const double g = (double)p.scratch[d * (d + 4) / 2 + 1];
+  const double N = p.sums[d + P + 1];
+  const int64_t co = col_off(d, k);
+  const int ab = a4_base(d, k);
+  for (int rr = threadIdx.x; rr < d - k; rr += 256) {
+    const int64_t o = co + rr;
+    if (ok) {
+      const double a = (1.0 - g) * p.in.cov[o];
+      const double b = g * (p.sums[d + o] / N);
+      p.out.cov[o] = a + b;
+      p.out.scale[o] = p.scratch[ab + k + rr];
+    } else {
+      p.out.cov[o] = p.in.cov[o];
+      p.out.scale[o] = p.in.scale[o];
+    }
+  }
 }
 
 // --------------------------------------------------------------- launchers --
@@ -539,7 +573,13 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
 
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
   const size_t shm = (size_t)p.d * (p.d + 4) / 2 * sizeof(float);
+  hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_big_update_kernel, dim3(1), dim3(1024), shm, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pooled_big_post_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

@@ -25,6 +25,8 @@ struct amh_handle {
   size_t partials_bytes = 0;
   float* split_buf = nullptr;  // split path: proposals [C][d] then U(z') [C] (scratch)
   size_t split_bytes = 0;
+  float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
+  size_t upd_bytes = 0;
   std::string err;
 };
 
@@ -130,6 +132,7 @@ int amh_destroy(amh_handle* h) {
     if (h->gamma_tab) (void)hipFree(h->gamma_tab);
     if (h->partials) (void)hipFree(h->partials);
     if (h->split_buf) (void)hipFree(h->split_buf);
+    if (h->upd_buf) (void)hipFree(h->upd_buf);
   }
   delete h;
   return AMH_OK;
@@ -513,7 +516,15 @@ int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state*
   p.sums = sums;
   p.in = *in;
   p.out = *out;
-  e = (p.d > 64) ? amh::run_pooled_big_update(p, (hipStream_t)stream) : amh::run_pooled_update(p, (hipStream_t)stream);
+  if (p.d > 64) {
+    const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 4) * sizeof(float);
+    int rc = grow(h, &h->upd_buf, &h->upd_bytes, need, stream, "amh_pooled_update/hipMalloc");
+    if (rc != AMH_OK) return rc;
+    p.scratch = h->upd_buf;
+    e = amh::run_pooled_big_update(p, (hipStream_t)stream);
+  } else {
+    e = amh::run_pooled_update(p, (hipStream_t)stream);
+  }
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update");
   return AMH_OK;
 }

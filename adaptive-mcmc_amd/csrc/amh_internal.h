@@ -103,6 +103,7 @@ struct PooledUpdateParams {
   float a, target;
   const double* sums;
   amh_pooled_state in, out;
+  float* scratch;  // d > 64: d(d+4)/2 floats (4-row-aligned factor) + ok flag
 };
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);

@@ -49,22 +49,25 @@ def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
     _run(kind, d, C, steps, gpu, orc)
 
 
-def test_pooled_inplace_multistep(gpu, orc):
-    """sample_ (amh_pooled_step, fused host loop) equals repeated sample()."""
+@pytest.mark.parametrize("d,C", [(16, 999), (128, 300), (256, 257)])
+def test_pooled_inplace_multistep(d, C, gpu, orc):
+    """sample_ (amh_pooled_step, in place: in and out states alias) equals
+    repeated out-of-place sample(); covers the large-d update's staging."""
     from kernels import PooledARWMH, PRNGKey
-    kw, mk, om = make_case("gaussian", 16)
-    C = 999
-    z0 = torch.empty(C, 16, device=gpu).uniform_(-2, 2)
+    kw, mk, om = make_case("gaussian", d)
+    z0 = torch.empty(C, d, device=gpu).uniform_(-2, 2)
     a = PooledARWMH(num_chains=C, **kw)
     sa = a.init(PRNGKey(4), 5, z0, (), mk)
     b = PooledARWMH(num_chains=C, **kw)
     sb = b.init(PRNGKey(4), 5, z0, (), mk)
+    assert d <= 64 or torch.equal(sa.cov, sb.cov)
     a.sample_(sa, 12)
     for _ in range(12):
         sb = b.sample(sb)
     torch.cuda.synchronize()
     assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
     assert torch.equal(sa.cov, sb.cov) and int(sa.i[0]) == 12
+    assert torch.equal(sa.adapt_state.loc, sb.adapt_state.loc) and torch.equal(sa.as_change, sb.as_change)
 
 
 def _gpu_worker(rank, world, port, C, steps, out_path):
