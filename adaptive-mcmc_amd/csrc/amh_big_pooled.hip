@@ -40,7 +40,7 @@ __global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsPara
   const int d = p.d;
   const int nt = d / 32;
   float* Xi = lds;  // [k][chain]: the noise, then e^lam L xi + eps xi
-  const int32_t it = p.i[0];
+  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
   const float el = amh_expf(p.lam[0]);
   const int64_t c0 = (int64_t)blockIdx.x * 64;
   for (int idx = threadIdx.x; idx < 64 * d; idx += 256) {
@@ -141,7 +141,7 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
   const int h = lane >> 5, i = lane & 31;
-  const int32_t it = p.i[0];
+  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
   const int64_t base = (int64_t)blockIdx.x * kBigChunk;
   const int part = blockIdx.y;
   const bool writer = part == 0;
@@ -302,8 +302,8 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const double N = sums[d + P + 1];
   const int32_t it = p.in.i[0];
-  const int32_t itr = it + 1;
-  const int32_t n = (it < p.W) ? itr : itr - p.W;
+  const int32_t itr = it + p.K;
+  const int32_t n = pooled_block_n(it, p.W, p.K);
   const float gamma = amh_lr_gamma(n, p.a);
   const float macc = p.in.mean_accept_prob[0];
   const float lam = p.in.log_step_size[0];
@@ -502,7 +502,7 @@ __global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const double N = p.sums[d + P + 1];
   const int32_t it = p.in.i[0];
-  const int32_t n = (it < p.W) ? it + 1 : it + 1 - p.W;
+  const int32_t n = pooled_block_n(it, p.W, p.K);
   const double g = (double)amh_lr_gamma(n, p.a);
   const int64_t co = col_off(d, k);
   const int ab = a4_base(d, k);
@@ -541,7 +541,8 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
 }
 
 // --------------------------------------------------------------- launchers --
-hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, hipStream_t s);
+hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
+                         hipStream_t s);
 
 int64_t pooled_big_chunks(int64_t C) { return (C + kBigChunk - 1) / kBigChunk; }
 
@@ -568,7 +569,7 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
                      ((size_t)d * kLd + 128) * sizeof(float), s, p, (const float*)xprop, (const float*)pep, per);
   e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return pooled_reduce(p.partials, nch, V, sums, s);
+  return pooled_reduce(p.partials, nch, V, sums, p.accumulate, s);
 }
 
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {

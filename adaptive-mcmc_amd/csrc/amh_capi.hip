@@ -448,11 +448,11 @@ int amh_pooled_sums_size(int32_t dim, int64_t* v) {
   return AMH_OK;
 }
 
-int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, float* z_out, float* pe_out,
-                     double* sums, void* stream) {
+int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
+                       float* z_out, float* pe_out, double* sums, void* stream) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_stats: null handle");
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
-  if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1)
+  if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1 || k_steps < 1)
     return fail(h, AMH_EINVAL, "amh_pooled_stats: bad arguments");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
@@ -488,13 +488,23 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
   p.pe_out = pe_out;
   p.partials = h->partials;
   p.model = h->model;
+  p.k_steps = k_steps;
   if (big) {
     const size_t nb = (size_t)num_chains * (size_t)(d + 1) * sizeof(float);
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;
-    e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
-                                  (hipStream_t)stream);
-    if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(d > 64)");
+    // one launch sequence per step of the block, the sums accumulated
+    for (int32_t t = 0; t < k_steps; ++t) {
+      p.i_add = t;
+      p.accumulate = t > 0;
+      if (t > 0) {
+        p.z = z_out;
+        p.pe = pe_out;
+      }
+      e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
+                                    (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(d > 64)");
+    }
     return AMH_OK;
   }
   e = amh::run_pooled_stats(h->model_id, p, sums, (hipStream_t)stream);
@@ -502,10 +512,17 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
   return AMH_OK;
 }
 
-int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
-                      void* stream) {
+int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, float* z_out, float* pe_out,
+                     double* sums, void* stream) {
+  return amh_pooled_stats_k(h, num_chains, in, 1, z_out, pe_out, sums, stream);
+}
+
+int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
+                        int32_t k_steps, void* stream) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_update: null handle");
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
+  if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
+    return fail(h, AMH_EINVAL, "amh_pooled_update: k_steps must be >= 1 and divide num_warmup");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipSetDevice");
   amh::PooledUpdateParams p{};
@@ -516,6 +533,7 @@ int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state*
   p.sums = sums;
   p.in = *in;
   p.out = *out;
+  p.K = k_steps;
   if (p.d > 64) {
     const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 4) * sizeof(float);
     int rc = grow(h, &h->upd_buf, &h->upd_bytes, need, stream, "amh_pooled_update/hipMalloc");
@@ -529,18 +547,29 @@ int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state*
   return AMH_OK;
 }
 
-int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, const amh_pooled_state* out,
-                    int32_t n_steps, double* sums, void* stream) {
-  if (n_steps < 0) return fail(h, AMH_EINVAL, "amh_pooled_step: n_steps < 0");
+int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
+                      void* stream) {
+  return amh_pooled_update_k(h, sums, in, out, 1, stream);
+}
+
+int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, const amh_pooled_state* out,
+                      int32_t n_steps, int32_t sync_every, double* sums, void* stream) {
+  if (n_steps < 0 || sync_every < 1 || n_steps % sync_every != 0)
+    return fail(h, AMH_EINVAL, "amh_pooled_step: n_steps must be a non-negative multiple of sync_every");
   const amh_pooled_state* src = in;
-  for (int32_t t = 0; t < n_steps; ++t) {
-    int rc = amh_pooled_stats(h, num_chains, src, out->z, out->potential_energy, sums, stream);
+  for (int32_t t = 0; t < n_steps; t += sync_every) {
+    int rc = amh_pooled_stats_k(h, num_chains, src, sync_every, out->z, out->potential_energy, sums, stream);
     if (rc != AMH_OK) return rc;
-    rc = amh_pooled_update(h, sums, src, out, stream);
+    rc = amh_pooled_update_k(h, sums, src, out, sync_every, stream);
     if (rc != AMH_OK) return rc;
     src = out;
   }
   return AMH_OK;
+}
+
+int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, const amh_pooled_state* out,
+                    int32_t n_steps, double* sums, void* stream) {
+  return amh_pooled_step_k(h, num_chains, in, out, n_steps, 1, sums, stream);
 }
 
 #ifdef AMH_STAMPS

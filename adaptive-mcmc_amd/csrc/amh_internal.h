@@ -96,7 +96,17 @@ struct PooledStatsParams {
   float *z_out, *pe_out;
   double* partials;  // [n_chunks][V]
   ModelArgs model;
+  int32_t k_steps;     // d <= 64: transitions per chain with the frozen shared state
+  int32_t i_add;       // d > 64: this launch is step i + i_add of the block
+  int32_t accumulate;  // d > 64: sums += this launch's sums (steps after the first)
 };
+
+// Pool-every-K: the update after a block of K transitions that started at
+// shared iteration it counts blocks, n = it / K + 1 (reset at W, W % K == 0);
+// K = 1 is arwmh.py:181.
+__host__ __device__ inline int32_t pooled_block_n(int32_t it, int32_t W, int32_t K) {
+  return (it < W) ? it / K + 1 : (it - W) / K + 1;
+}
 
 struct PooledUpdateParams {
   int32_t d, W;
@@ -104,6 +114,7 @@ struct PooledUpdateParams {
   const double* sums;
   amh_pooled_state in, out;
   float* scratch;  // d > 64: d(d+4)/2 floats (4-row-aligned factor) + ok flag
+  int32_t K;       // transitions per pooled update (the sums cover K * C chain-steps)
 };
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);

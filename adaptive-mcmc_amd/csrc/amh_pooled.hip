@@ -124,42 +124,48 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
   float zq = 0.0f, peq = 0.0f;
   uint32_t k0q = 0, k1q = 0;
   if (base < end) load_chain(base, zq, peq, k0q, k1q);
+  const int K = p.k_steps;
   for (int64_t c = base; c < end; ++c) {
-    const float z = zq, pe = peq;
+    float z = zq, pe = peq;
     const uint32_t k0 = k0q, k1 = k1q;
     if (c + 1 < end) load_chain(c + 1, zq, peq, k0q, k1q);
-    // noise at the shared stream position (arwmh.py:162-165, 174)
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-    const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
-    const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
-    // proposal with the shared factor (arwmh.py:166-167)
-    const float acc = lds_row_dot64(prow, d, xi, act);
-    const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
-    float pep = M<G>::potential(zp, r, d, mctx, lds);
-    if (amh_isnan(pep)) pep = INFINITY;
-    const float ex = amh_expf(pe - pep);
-    const float alpha = (ex > 1.0f) ? 1.0f : ex;
-    const bool accept = u < alpha;
-    const float zn = accept ? zp : z;
+    // K transitions with the frozen shared state (K = 1: one pooled step)
+    for (int t = 0; t < K; ++t) {
+      // noise at the shared stream position i + t (arwmh.py:162-165, 174)
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)(it + t), 0u, AMH_TAG_STEP, k0, k1);
+      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      // proposal with the shared factor (arwmh.py:166-167)
+      const float acc = lds_row_dot64(prow, d, xi, act);
+      const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+      float pep = M<G>::potential(zp, r, d, mctx, lds);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      const bool accept = u < alpha;
+      z = accept ? zp : z;
+      pe = accept ? pep : pe;
+      // pooled statistics (float32 over this wave's chain-steps: chains in
+      // order, each chain's K steps in order)
+      const float delta = act ? z - mu : 0.0f;
+      sd = sd + delta;
+      // (S_k, S_k+1) += delta_r (delta_k, delta_k+1): one v_pk_fma_f32 per pair
+      // (each half is the same fmaf; past d the broadcast delta is 0)
+      static_for<32>([&](auto K2) {
+        constexpr int k = 2 * K2;
+        if (k < d) {
+          const f32x2v bp = {Gp::template bcast<k>(delta), Gp::template bcast<k + 1>(delta)};
+          const f32x2v sp = __builtin_elementwise_fma(f32x2v{delta, delta}, bp, f32x2v{S[k], S[k + 1]});
+          S[k] = sp[0];
+          S[k + 1] = sp[1];
+        }
+        column_fence<k + 1>();
+      });
+      sa = sa + alpha;
+    }
     const Buf bo(uniform_ptr(p.z_out + c * d), 4u * (uint32_t)d);
-    bo.st(zn, vr, 0);
-    if (r == 0) p.pe_out[c] = accept ? pep : pe;
-    // pooled statistics (float32 over this wave's chains, in chain order)
-    const float delta = act ? zn - mu : 0.0f;
-    sd = sd + delta;
-    // (S_k, S_k+1) += delta_r (delta_k, delta_k+1): one v_pk_fma_f32 per pair
-    // (each half is the same fmaf; past d the broadcast delta is 0)
-    static_for<32>([&](auto K2) {
-      constexpr int k = 2 * K2;
-      if (k < d) {
-        const f32x2v bp = {Gp::template bcast<k>(delta), Gp::template bcast<k + 1>(delta)};
-        const f32x2v sp = __builtin_elementwise_fma(f32x2v{delta, delta}, bp, f32x2v{S[k], S[k + 1]});
-        S[k] = sp[0];
-        S[k + 1] = sp[1];
-      }
-      column_fence<k + 1>();
-    });
-    sa = sa + alpha;
+    bo.st(z, vr, 0);
+    if (r == 0) p.pe_out[c] = pe;
   }
   // The chunk's 16 wave partials are combined by a fixed pairwise tree in
   // float32 (h = 8, 4, 2, 1: wave w < h adds wave w + h), through LDS slots
@@ -205,7 +211,7 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
     if (lane == 0) {
       const int64_t left = p.C - chunk0;
       out[d + P] = (double)sa;
-      out[d + P + 1] = (double)(left < (int64_t)kPoolWaves * cpw ? left : (int64_t)kPoolWaves * cpw);
+      out[d + P + 1] = (double)K * (double)(left < (int64_t)kPoolWaves * cpw ? left : (int64_t)kPoolWaves * cpw);
     }
   }
 }
@@ -218,7 +224,7 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
 constexpr int kRedGroup = 16;
 
 __global__ __launch_bounds__(1024) void pooled_reduce_kernel(const double* partials, int64_t n_chunks, int64_t V,
-                                                             double* sums) {
+                                                             double* sums, int accumulate) {
   __shared__ double gs[16][64];
   const int tv = threadIdx.x & 63;
   const int q = threadIdx.x >> 6;
@@ -239,12 +245,13 @@ __global__ __launch_bounds__(1024) void pooled_reduce_kernel(const double* parti
     }
     __syncthreads();
   }
-  if (q == 0 && v < V) sums[v] = tot;
+  if (q == 0 && v < V) sums[v] = accumulate ? sums[v] + tot : tot;
 }
 
-hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, hipStream_t s) {
+hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
+                         hipStream_t s) {
   hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, partials, n_chunks, V,
-                     sums);
+                     sums, accumulate);
   return hipGetLastError();
 }
 
@@ -272,8 +279,8 @@ __global__ __launch_bounds__(512) void pooled_update_kernel(PooledUpdateParams p
   const double* sums = p.sums;
   const double N = sums[d + P + 1];
   const int32_t it = p.in.i[0];
-  const int32_t itr = it + 1;
-  const int32_t n = (it < p.W) ? itr : itr - p.W;
+  const int32_t itr = it + p.K;
+  const int32_t n = pooled_block_n(it, p.W, p.K);
   const float gamma = amh_lr_gamma(n, p.a);
   const double g = (double)gamma;
   __shared__ double As[64 * kUpdLd];  // Sigma' [r][k], then the new factor (float view)
@@ -400,7 +407,7 @@ hipError_t launch_pooled_stats(const PooledStatsParams& p, double* sums, hipStre
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, p.partials,
-                     n_chunks, V, sums);
+                     n_chunks, V, sums, 0);
   return hipGetLastError();
 }
 

@@ -24,7 +24,8 @@ AMH_MODEL_DIAMONDS = 4
 # every symbol include/amh.h declares
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",
            "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
-           "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_asss_step",
+           "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
+           "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
            "amh_normals")
 

@@ -45,7 +45,11 @@ def _bind_pooled(L):
     L.amh_pooled_stats.argtypes = [P, I64, PS, P, P, P, P]
     L.amh_pooled_update.argtypes = [P, P, PS, PS, P]
     L.amh_pooled_step.argtypes = [P, I64, PS, PS, I32, P, P]
-    for n in ("amh_pooled_sums_size", "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step"):
+    L.amh_pooled_stats_k.argtypes = [P, I64, PS, I32, P, P, P]
+    L.amh_pooled_update_k.argtypes = [P, P, PS, PS, I32, P]
+    L.amh_pooled_step_k.argtypes = [P, I64, PS, PS, I32, I32, P, P]
+    for n in ("amh_pooled_sums_size", "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step",
+              "amh_pooled_stats_k", "amh_pooled_update_k", "amh_pooled_step_k"):
         getattr(L, n).restype = ctypes.c_int
     L._pooled_bound = True
     return L
@@ -60,17 +64,27 @@ class PooledARWMH(ARWMH):
 
     Same constructor and init arguments as ARWMH; `group` is the
     torch.distributed process group whose chains are pooled (default: the
-    default group when initialised, else this process alone)."""
+    default group when initialised, else this process alone).
+
+    sync_every = K pools every K transitions: the shared
+    state is frozen for a block of K transitions of every chain, the sums
+    (and, across ranks, the one all-reduce) cover the block's K * C
+    chain-steps, and one update ends it, with gamma counting blocks.  Then
+    `sample` advances one block and `sample_(n)` needs n % K == 0;
+    num_warmup must be a multiple of K."""
 
     pooled = True  # adapt-state leaves carry no chain axis
 
     def __init__(self, model=None, potential_fn=None, lr_decay=2 / 3, target_accept_prob=0.234, eps=1e-6,
-                 num_chains=None, device=None, chain_offset=0, group=None, **kw):
+                 num_chains=None, device=None, chain_offset=0, group=None, sync_every: int = 1, **kw):
         super().__init__(model=model, potential_fn=potential_fn, lr_decay=lr_decay,
                          target_accept_prob=target_accept_prob, eps=eps, num_chains=num_chains, device=device,
                          chain_offset=chain_offset, **kw)
+        if int(sync_every) < 1:
+            raise ValueError("sync_every must be >= 1")
         self._group = group
         self._sums = None
+        self.sync_every = int(sync_every)
 
     def _world(self) -> int:
         if not dist.is_available() or not dist.is_initialized():
@@ -81,6 +95,8 @@ class PooledARWMH(ARWMH):
         """Per-chain z0 / pe0 / keys as ARWMH.init (arwmh.py:84-138); shared
         state mu = 0, L = Sigma = I, lambda = 0, i = 0 (mu_0 is irrelevant
         after step 1, where gamma_1 = 1)."""
+        if int(num_warmup) % self.sync_every != 0:
+            raise ValueError(f"num_warmup ({num_warmup}) must be a multiple of sync_every ({self.sync_every})")
         st = super().init(rng_key, num_warmup, init_params, model_args, model_kwargs)
         d, dev = self._dim, st.z.device
         f = dict(dtype=torch.float32, device=dev)
@@ -128,35 +144,40 @@ class PooledARWMH(ARWMH):
         dev = sin.z.device.index
         C = sin.z.shape[0]
         cin, cout = self._c(sin), self._c(sout)
+        K = self.sync_every
         with torch.cuda.device(dev):
             stream = _lib.stream_ptr(dev)
-            _lib.check(L.amh_pooled_stats(self._handle.h, C, ctypes.byref(cin), _lib.ptr(sout.z),
-                                          _lib.ptr(sout.potential_energy), _lib.ptr(self._sums), stream),
+            _lib.check(L.amh_pooled_stats_k(self._handle.h, C, ctypes.byref(cin), K, _lib.ptr(sout.z),
+                                            _lib.ptr(sout.potential_energy), _lib.ptr(self._sums), stream),
                        self._handle.h)
             if self._world() > 1:
                 dist.all_reduce(self._sums, op=dist.ReduceOp.SUM, group=self._group)
-            _lib.check(L.amh_pooled_update(self._handle.h, _lib.ptr(self._sums), ctypes.byref(cin),
-                                           ctypes.byref(cout), stream), self._handle.h)
+            _lib.check(L.amh_pooled_update_k(self._handle.h, _lib.ptr(self._sums), ctypes.byref(cin),
+                                             ctypes.byref(cout), K, stream), self._handle.h)
 
     def sample(self, state, model_args=(), model_kwargs=None):
-        """One pooled transition of every chain; returns a new state."""
+        """One pooled transition of every chain (sync_every > 1: one block of
+        them); returns a new state."""
         self._check(state)
         out = self._new_like(state)
         self._one(state, out)
         return out
 
     def sample_(self, state, n_steps: int = 1):
-        """n_steps pooled transitions in place."""
+        """n_steps pooled transitions in place (a multiple of sync_every)."""
         C = self._check(state)
+        K = self.sync_every
+        if int(n_steps) % K != 0:
+            raise ValueError(f"n_steps ({n_steps}) must be a multiple of sync_every ({K})")
         if self._world() == 1:
             L = _bind_pooled(_lib.lib())
             dev = state.z.device.index
             c = self._c(state)
             with torch.cuda.device(dev):
-                _lib.check(L.amh_pooled_step(self._handle.h, C, ctypes.byref(c), ctypes.byref(c), int(n_steps),
-                                             _lib.ptr(self._sums), _lib.stream_ptr(dev)), self._handle.h)
+                _lib.check(L.amh_pooled_step_k(self._handle.h, C, ctypes.byref(c), ctypes.byref(c), int(n_steps), K,
+                                               _lib.ptr(self._sums), _lib.stream_ptr(dev)), self._handle.h)
             return state
-        for _ in range(int(n_steps)):
+        for _ in range(int(n_steps) // K):
             self._one(state, state)
         return state
 

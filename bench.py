@@ -57,14 +57,17 @@ def measured_traffic(C: int, d: int):
     return best
 
 
-def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int):
+def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int, sync_every: int = 1):
     """Regime B (pooled covariance, BASELINE.json configs[4] at N = 8): every
     step = per-chain transition + local sums, all-reduce(sum) of the sums over
-    RCCL (world > 1), shared refactorisation on every rank."""
+    RCCL (world > 1), shared refactorisation on every rank.  sync_every = K:
+    one all-reduce and refactorisation per K transitions."""
     import torch
     import torch.distributed as dist
     from kernels import PooledARWMH, PRNGKey
-    k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=rank * C)
+    K = sync_every
+    steps, warmup = -(-steps // K) * K, -(-warmup // K) * K
+    k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=rank * C, sync_every=K)
     gen = torch.Generator(device=dev)
     gen.manual_seed(99 + rank)
     z0 = (torch.rand(C, g.dim, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
@@ -85,8 +88,8 @@ def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int)
         wall = float(t.item())
     return {"value": world * C * steps / wall, "unit": "chain-steps/s", "ms_per_step": wall / steps * 1e3,
             "steps": steps, "chains_per_gpu": C, "allreduce_doubles": g.dim + g.dim * (g.dim + 1) // 2 + 2,
-            "mean_accept_prob": float(st.mean_accept_prob[0]),
-            "collective": "all_reduce(sum) per step" if world > 1 else "none (1 rank)"}
+            "mean_accept_prob": float(st.mean_accept_prob[0]), "sync_every": K,
+            "collective": (f"all_reduce(sum) per {K} step(s)" if world > 1 else "none (1 rank)")}
 
 
 def cpu_baseline(g, d: int, budget_s: float = 12.0):
@@ -211,6 +214,8 @@ def main():
     pooled = None
     if not args.no_pooled:
         pooled = bench_pooled(g, C, dev, rank, world, steps=max(args.steps, 20), warmup=5)
+        pooled["sync_every_16"] = bench_pooled(g, C, dev, rank, world, steps=max(args.steps, 32), warmup=16,
+                                               sync_every=16)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

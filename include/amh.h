@@ -211,6 +211,21 @@ int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state*
 int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in,
                     const amh_pooled_state* out, int32_t n_steps, double* sums, void* stream);
 
+/* Pool every K steps (one exchange per K transitions).  The
+ * shared state stays frozen for a block of K transitions of every chain
+ * (noise positions i .. i+K-1), the sums cover all K * C chain-steps (delta
+ * against the frozen mu, N = K * C), and one update ends the block: i += K,
+ * gamma = 1 / n^a with n = the block count (i / K + 1, reset at num_warmup,
+ * which must be a multiple of K).  K = 1 is amh_pooled_stats / _update. */
+int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
+                       float* z_out, float* pe_out, double* sums, void* stream);
+int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_state* in,
+                        const amh_pooled_state* out, int32_t k_steps, void* stream);
+/* n_steps (a multiple of sync_every) transitions, one update per sync_every. */
+int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in,
+                      const amh_pooled_state* out, int32_t n_steps, int32_t sync_every, double* sums,
+                      void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -622,15 +622,28 @@ static float orc_potential_g(const orc_cfg* cfg, const float* x, int G) {
 static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
                                  const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
                                  float* z_out, float* pe_out, double* sums);
-static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
-                                 float* Lpacked, float* lam, float* asc, double* cov);
+static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t K, int32_t* i_, float* macc,
+                                 float* mu, float* Lpacked, float* lam, float* asc, double* cov);
 
-void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
-                      const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
-                      float* z_out, float* pe_out, double* sums) {
+/* Pool every K (amh_pooled_stats_k): K transitions per chain with the frozen
+ * shared state at noise positions i .. i+K-1, the sums over all K*C
+ * chain-steps.  d <= 64: one kernel, each wave's chains in order with each
+ * chain's K steps in order.  d > 64: K launch sequences, sums accumulated
+ * in step order (sums = s_0, then sums + s_t). */
+void orc_pooled_stats_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, const float* z, const float* pe,
+                        const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
+                        float* z_out, float* pe_out, double* sums) {
   const int d = cfg->d;
   if (d > ORC_DMAX) {
-    orc_pooled_stats_big(cfg, C, i, z, pe, keys, mu, Lpacked, lam, z_out, pe_out, sums);
+    const int64_t V = d + packed_size(d) + 2;
+    double* tmp = (double*)malloc((size_t)V * sizeof(double));
+    for (int32_t t = 0; t < K; ++t) {
+      orc_pooled_stats_big(cfg, C, i + t, t ? z_out : z, t ? pe_out : pe, keys, mu, Lpacked, lam, z_out, pe_out,
+                           t ? tmp : sums);
+      if (t)
+        for (int64_t v = 0; v < V; ++v) sums[v] = sums[v] + tmp[v];
+    }
+    free(tmp);
     return;
   }
   const int64_t P = packed_size(d);
@@ -657,38 +670,43 @@ void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, 
       for (int t = 0; t < cpw; ++t) {
         const int64_t c = ch * chunk + (int64_t)w * cpw + t;
         if (c >= C) continue;
-        cnt += 1.0;
         const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
-        float xi[ORC_DMAX], zp[ORC_DMAX], zn[ORC_DMAX], delta[ORC_DMAX];
-        uint32_t ubits = 0;
-        for (int r = 0; r < d; ++r) {
-          const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)i, 0u, AMH_TAG_STEP, k0, k1);
-          xi[r] = amh_normal_from_bits(o.v[0]);
-          if (r == 0) ubits = o.v[1];
+        float zc[ORC_DMAX], pec = pe[c];
+        for (int r = 0; r < d; ++r) zc[r] = z[c * d + r];
+        for (int32_t s = 0; s < K; ++s) {
+          cnt += 1.0;
+          float xi[ORC_DMAX], zp[ORC_DMAX], delta[ORC_DMAX];
+          uint32_t ubits = 0;
+          for (int r = 0; r < d; ++r) {
+            const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)(i + s), 0u, AMH_TAG_STEP, k0, k1);
+            xi[r] = amh_normal_from_bits(o.v[0]);
+            if (r == 0) ubits = o.v[1];
+          }
+          const float u = amh_unif01_from_bits(ubits);
+          for (int r = 0; r < d; ++r) {
+            float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            for (int j = 0; j < d; ++j) a4[j & 3] = fmaf(L[r][j], xi[j], a4[j & 3]);
+            const float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+            zp[r] = zc[r] + fmaf(el, a, cfg->eps * xi[r]);
+          }
+          float pep = orc_potential_g(cfg, zp, 64);
+          if (amh_isnan(pep)) pep = INFINITY;
+          const float ex = amh_expf(pec - pep);
+          const float alpha = (ex > 1.0f) ? 1.0f : ex;
+          const int accept = u < alpha;
+          for (int r = 0; r < d; ++r) {
+            zc[r] = accept ? zp[r] : zc[r];
+            delta[r] = zc[r] - mu[r];
+          }
+          pec = accept ? pep : pec;
+          for (int r = 0; r < d; ++r) {
+            sd[w][r] = sd[w][r] + delta[r];
+            for (int k = 0; k <= r; ++k) S[w][r][k] = fmaf(delta[r], delta[k], S[w][r][k]);
+          }
+          sa[w] = sa[w] + alpha;
         }
-        const float u = amh_unif01_from_bits(ubits);
-        for (int r = 0; r < d; ++r) {
-          float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-          for (int j = 0; j < d; ++j) a4[j & 3] = fmaf(L[r][j], xi[j], a4[j & 3]);
-          const float a = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-          zp[r] = z[c * d + r] + fmaf(el, a, cfg->eps * xi[r]);
-        }
-        float pep = orc_potential_g(cfg, zp, 64);
-        if (amh_isnan(pep)) pep = INFINITY;
-        const float ex = amh_expf(pe[c] - pep);
-        const float alpha = (ex > 1.0f) ? 1.0f : ex;
-        const int accept = u < alpha;
-        for (int r = 0; r < d; ++r) {
-          zn[r] = accept ? zp[r] : z[c * d + r];
-          delta[r] = zn[r] - mu[r];
-        }
-        for (int r = 0; r < d; ++r) {
-          z_out[c * d + r] = zn[r];
-          sd[w][r] = sd[w][r] + delta[r];
-          for (int k = 0; k <= r; ++k) S[w][r][k] = fmaf(delta[r], delta[k], S[w][r][k]);
-        }
-        pe_out[c] = accept ? pep : pe[c];
-        sa[w] = sa[w] + alpha;
+        for (int r = 0; r < d; ++r) z_out[c * d + r] = zc[r];
+        pe_out[c] = pec;
       }
     }
     /* pairwise tree over the 16 waves (h = 8, 4, 2, 1), float32 */
@@ -722,17 +740,26 @@ void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, 
   free(part);
 }
 
+void orc_pooled_stats(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
+                      const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
+                      float* z_out, float* pe_out, double* sums) {
+  orc_pooled_stats_k(cfg, C, i, 1, z, pe, keys, mu, Lpacked, lam, z_out, pe_out, sums);
+}
+
 /* Shared-state update from the (all-reduced) sums.  Returns 1 if the factor
  * was refactorised, 0 if kept. */
-int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
-                      float* Lpacked, float* lam, float* asc, double* cov) {
+/* the block counter of amh_internal.h pooled_block_n: n = it / K + 1 (reset at W) */
+static int32_t orc_block_n(int32_t it, int32_t W, int32_t K) { return (it < W) ? it / K + 1 : (it - W) / K + 1; }
+
+int orc_pooled_update_k(const orc_cfg* cfg, const double* sums, int32_t K, int32_t* i_, float* macc, float* mu,
+                        float* Lpacked, float* lam, float* asc, double* cov) {
   const int d = cfg->d;
-  if (d > ORC_DMAX) return orc_pooled_update_big(cfg, sums, i_, macc, mu, Lpacked, lam, asc, cov);
+  if (d > ORC_DMAX) return orc_pooled_update_big(cfg, sums, K, i_, macc, mu, Lpacked, lam, asc, cov);
   const int64_t P = packed_size(d);
   const double N = sums[d + P + 1];
   const int32_t it = *i_;
-  const int32_t itr = it + 1;
-  const int32_t n = (it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const int32_t itr = it + K;
+  const int32_t n = orc_block_n(it, cfg->num_warmup, K);
   const float gamma = amh_lr_gamma(n, cfg->lr_decay);
   const float abar = (float)(sums[d + P] / N);
   const float maccn = *macc + (abar - *macc) / (float)n;
@@ -787,6 +814,11 @@ int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float
   *macc = maccn;
   *lam = lamn;
   return ok;
+}
+
+int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
+                      float* Lpacked, float* lam, float* asc, double* cov) {
+  return orc_pooled_update_k(cfg, sums, 1, i_, macc, mu, Lpacked, lam, asc, cov);
 }
 
 /* ====================================== large dimensions (64 < d <= 256) ==== */
@@ -1099,14 +1131,14 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
   free(part);
 }
 
-static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t* i_, float* macc, float* mu,
-                                 float* Lpacked, float* lam, float* asc, double* cov) {
+static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t K, int32_t* i_, float* macc,
+                                 float* mu, float* Lpacked, float* lam, float* asc, double* cov) {
   const int d = cfg->d;
   const int64_t P = packed_size(d);
   const double N = sums[d + P + 1];
   const int32_t it = *i_;
-  const int32_t itr = it + 1;
-  const int32_t n = (it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const int32_t itr = it + K;
+  const int32_t n = orc_block_n(it, cfg->num_warmup, K);
   const float gamma = amh_lr_gamma(n, cfg->lr_decay);
   const float abar = (float)(sums[d + P] / N);
   const float maccn = *macc + (abar - *macc) / (float)n;

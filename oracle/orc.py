@@ -80,6 +80,9 @@ def lib():
         L.orc_pooled_stats.argtypes = [_P, _I64, _I32, _P, _P, _P, _P, _P, _F, _P, _P, _P]
         L.orc_pooled_update.argtypes = [_P, _P] + [_P] * 7
         L.orc_pooled_update.restype = ctypes.c_int
+        L.orc_pooled_stats_k.argtypes = [_P, _I64, _I32, _I32, _P, _P, _P, _P, _P, _F, _P, _P, _P]
+        L.orc_pooled_update_k.argtypes = [_P, _P, _I32] + [_P] * 7
+        L.orc_pooled_update_k.restype = ctypes.c_int
         _lib = L
     return _lib
 
@@ -253,8 +256,9 @@ def pooled_cpw(C: int) -> int:
     return lib().orc_pooled_cpw(C)
 
 
-def pooled_stats(model: Model, i: int, z, pe, keys, mu, Lpacked, lam: float, eps: float = 1e-6):
-    """-> (z_out, pe_out, sums[V]) for one pooled step (orc_pooled_stats)."""
+def pooled_stats(model: Model, i: int, z, pe, keys, mu, Lpacked, lam: float, eps: float = 1e-6, k_steps: int = 1):
+    """-> (z_out, pe_out, sums[V]) for one pooled step, or a block of k_steps
+    transitions with the frozen shared state (orc_pooled_stats_k)."""
     d = model.d
     z = _c(z, np.float32).reshape(-1, d)
     C = z.shape[0]
@@ -266,21 +270,21 @@ def pooled_stats(model: Model, i: int, z, pe, keys, mu, Lpacked, lam: float, eps
     po = np.empty_like(pe)
     sums = np.empty(d + d * (d + 1) // 2 + 2, np.float64)
     cfg = model.cfg(0, 2 / 3, 0.234, eps)
-    lib().orc_pooled_stats(ctypes.byref(cfg), C, int(i), _ptr(z), _ptr(pe), _ptr(keys), _ptr(mu), _ptr(Lp),
-                           ctypes.c_float(lam), _ptr(zo), _ptr(po), _ptr(sums))
+    lib().orc_pooled_stats_k(ctypes.byref(cfg), C, int(i), int(k_steps), _ptr(z), _ptr(pe), _ptr(keys), _ptr(mu),
+                             _ptr(Lp), ctypes.c_float(lam), _ptr(zo), _ptr(po), _ptr(sums))
     return zo, po, sums
 
 
 def pooled_update(model: Model, sums, shared: dict, num_warmup: int = 0, lr_decay: float = 2 / 3,
-                  target_accept_prob: float = 0.234) -> int:
+                  target_accept_prob: float = 0.234, k_steps: int = 1) -> int:
     """In-place update of shared = {i, macc, mu, L, lam, asc, cov} (numpy
     arrays: i int32[1], macc/lam/asc float32[1], mu float32[d], L float32[P],
     cov float64[P]).  Returns 1 if refactorised."""
     cfg = model.cfg(num_warmup, lr_decay, target_accept_prob, 1e-6)
     sums = _c(sums, np.float64)
-    return lib().orc_pooled_update(ctypes.byref(cfg), _ptr(sums), _ptr(shared["i"]), _ptr(shared["macc"]),
-                                   _ptr(shared["mu"]), _ptr(shared["L"]), _ptr(shared["lam"]), _ptr(shared["asc"]),
-                                   _ptr(shared["cov"]))
+    return lib().orc_pooled_update_k(ctypes.byref(cfg), _ptr(sums), int(k_steps), _ptr(shared["i"]),
+                                     _ptr(shared["macc"]), _ptr(shared["mu"]), _ptr(shared["L"]), _ptr(shared["lam"]),
+                                     _ptr(shared["asc"]), _ptr(shared["cov"]))
 
 
 def pooled_init_shared(d: int) -> dict:

@@ -10,10 +10,10 @@ from helpers import make_case
 pytestmark = pytest.mark.gpu
 
 
-def _run(kind, d, C, steps, gpu, orc, seed=0):
+def _run(kind, d, C, steps, gpu, orc, seed=0, K=1):
     from kernels import PooledARWMH, PRNGKey
     kw, mk, om = make_case(kind, d)
-    k = PooledARWMH(num_chains=C, **kw)
+    k = PooledARWMH(num_chains=C, sync_every=K, **kw)
     z0 = np.random.default_rng(seed).uniform(-2, 2, size=(C, om.d)).astype(np.float32)
     st = k.init(PRNGKey(seed), 0, torch.as_tensor(z0), (), mk)
     ost = orc.init(om, PRNGKey(seed), C, init_z=z0)
@@ -23,11 +23,12 @@ def _run(kind, d, C, steps, gpu, orc, seed=0):
     sh = orc.pooled_init_shared(om.d)
     for t in range(steps):
         st = k.sample(st)
-        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
         torch.cuda.synchronize()
         np.testing.assert_array_equal(k._sums.cpu().numpy().view(np.uint64), sums.view(np.uint64),
                                       err_msg=f"{kind} sums step {t + 1}")
-        orc.pooled_update(om, sums, sh)
+        orc.pooled_update(om, sums, sh, k_steps=K)
         got = dict(z=st.z, pe=st.potential_energy, mu=st.adapt_state.loc, L=st.adapt_state.scale,
                    lam=st.adapt_state.log_step_size, macc=st.mean_accept_prob, asc=st.as_change, cov=st.cov,
                    i=st.i)
@@ -68,6 +69,38 @@ def test_pooled_inplace_multistep(d, C, gpu, orc):
     assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
     assert torch.equal(sa.cov, sb.cov) and int(sa.i[0]) == 12
     assert torch.equal(sa.adapt_state.loc, sb.adapt_state.loc) and torch.equal(sa.as_change, sb.as_change)
+
+
+@pytest.mark.parametrize("kind,d,C,blocks,K", [("gaussian", 64, 3000, 3, 4), ("gaussian", 64, 70000, 2, 16),
+                                               ("gaussian", 7, 517, 3, 5), ("eight_schools", None, 64, 3, 16),
+                                               ("diamonds", None, 40, 2, 3), ("gaussian", 128, 700, 2, 3),
+                                               ("gaussian", 256, 600, 2, 2)])
+def test_pooled_blocks_bitexact(kind, d, C, blocks, K, gpu, orc):
+    """sync_every = K (one update per K transitions): per-chain state, the
+    block's sums and the shared state bit for bit against orc_pooled_*_k."""
+    _run(kind, d, C, blocks, gpu, orc, K=K)
+
+
+@pytest.mark.parametrize("d,C,K", [(16, 999, 4), (128, 300, 3)])
+def test_pooled_blocks_inplace(d, C, K, gpu, orc):
+    """sample_(12) with sync_every = K in place (amh_pooled_step_k) equals
+    12 / K out-of-place block samples."""
+    from kernels import PooledARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", d)
+    z0 = torch.empty(C, d, device=gpu).uniform_(-2, 2)
+    a = PooledARWMH(num_chains=C, sync_every=K, **kw)
+    sa = a.init(PRNGKey(4), 0, z0, (), mk)
+    b = PooledARWMH(num_chains=C, sync_every=K, **kw)
+    sb = b.init(PRNGKey(4), 0, z0, (), mk)
+    a.sample_(sa, 12)
+    for _ in range(12 // K):
+        sb = b.sample(sb)
+    torch.cuda.synchronize()
+    assert int(sa.i[0]) == 12 and int(sb.i[0]) == 12
+    assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
+    assert torch.equal(sa.cov, sb.cov) and torch.equal(sa.adapt_state.loc, sb.adapt_state.loc)
+    with pytest.raises(ValueError):
+        a.sample_(sa, 5 if K != 5 else 7)
 
 
 def _gpu_worker(rank, world, port, C, steps, out_path):

@@ -175,3 +175,125 @@ def test_one_chain_big_is_the_reference_recurrence(d, orc):
         L1 = _unpack(sh["L"], d)
         Lr = ref.adapt_state.scale
         assert np.max(np.abs(L1 @ L1.T - Lr @ Lr.T)) <= 1e-3 * np.max(np.abs(Lr @ Lr.T)) + 1e-5, f"step {t + 1}"
+
+
+# ------------------------------------------------ pool every K (sync_every) --
+def _shared_copy(sh):
+    return {k: v.copy() for k, v in sh.items()}
+
+
+@pytest.mark.parametrize("kind,d,C,K", [("gaussian", 12, 37, 4), ("eight_schools", None, 70, 3),
+                                        ("gaussian", 128, 40, 3)])
+def test_block_is_k_frozen_steps(kind, d, C, K, orc):
+    """A block of K transitions (orc_pooled_stats_k) is K single pooled steps
+    with the shared state frozen: per-chain z / pe bit for bit, the sums equal
+    up to association order (d <= 64: one float32 accumulator per wave over
+    all K steps; d > 64: the per-step sums added in step order, exactly)."""
+    from helpers import make_case
+    from kernels import PRNGKey
+    _, _, om = make_case(kind, d)
+    st = orc.init(om, PRNGKey(3), C)
+    z, pe, keys = st.z, st.potential_energy, st.rng_key
+    sh = orc.pooled_init_shared(om.d)
+    for _ in range(3):  # move off the identity first
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        orc.pooled_update(om, sums, sh)
+    i0 = int(sh["i"][0])
+    zb, peb, sb = orc.pooled_stats(om, i0, z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]), k_steps=K)
+    tot = None
+    for t in range(K):
+        z, pe, s = orc.pooled_stats(om, i0 + t, z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        tot = s.copy() if tot is None else tot + s
+    assert zb.tobytes() == z.tobytes() and peb.tobytes() == pe.tobytes()
+    assert sb[-1] == K * C
+    if om.d > 64:
+        assert sb.tobytes() == tot.tobytes()
+    else:
+        np.testing.assert_allclose(sb, tot, rtol=2e-5, atol=1e-6 * np.abs(tot).max())
+
+
+def test_block_update_counts_blocks(orc):
+    """update_k: i advances by K; gamma = 1/n^a with n the block count
+    (i / K + 1), reset at num_warmup; K = 1 is the per-step rule."""
+    from helpers import make_case
+    from kernels import PRNGKey
+    K, W, C, a = 4, 8, 50, 2 / 3
+    _, _, om = make_case("gaussian", 6)
+    st = orc.init(om, PRNGKey(1), C)
+    z, pe, keys = st.z, st.potential_energy, st.rng_key
+    sh = orc.pooled_init_shared(om.d)
+    for blk in range(4):
+        i = int(sh["i"][0])
+        n = (i // K + 1) if i < W else ((i - W) // K + 1)
+        z, pe, sums = orc.pooled_stats(om, i, z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]), k_steps=K)
+        before = _shared_copy(sh)
+        orc.pooled_update(om, sums, sh, num_warmup=W, k_steps=K)
+        assert int(sh["i"][0]) == i + K
+        gamma = float(orc.lr_gamma([n], a)[0])
+        mu = before["mu"] + np.float32(gamma) * (sums[:6] / sums[-1]).astype(np.float32)
+        np.testing.assert_array_equal(sh["mu"], mu)
+        P = 21
+        S = (1 - gamma) * before["cov"] + gamma * (sums[6:6 + P] / sums[-1])
+        np.testing.assert_allclose(sh["cov"], S, rtol=1e-12)
+    assert int(sh["i"][0]) == 4 * K
+
+
+def _pooled_block_worker(rank, world, port, C, steps, K, out_path):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import orc
+    from helpers import make_case
+    from kernels import PRNGKey
+    from kernels.distributed import gather_chains, shard_range
+    _, _, om = make_case("gaussian", 12)
+    off, cnt = shard_range(C, rank, world)
+    st = orc.init(om, PRNGKey(9), cnt, chain_offset=off)
+    z, pe, keys = st.z, st.potential_energy, st.rng_key
+    sh = orc.pooled_init_shared(om.d)
+    for _ in range(steps // K):
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
+        t = torch.from_numpy(sums.copy())
+        dist.all_reduce(t)  # one exchange per K transitions
+        orc.pooled_update(om, t.numpy(), sh, k_steps=K)
+    zall = gather_chains(torch.from_numpy(z), C).numpy()
+    if rank == 0:
+        np.savez(out_path, z=zall, L=sh["L"], mu=sh["mu"], i=sh["i"])
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_match_one_blocks(tmp_path, orc):
+    """sync_every = 4 over 2 gloo ranks (one all-reduce per block) equals the
+    single-process block run up to the association order of the sums."""
+    from helpers import make_case
+    from kernels import PRNGKey
+    C, steps, K = 301, 40, 4
+    out = str(tmp_path / "pb.npz")
+    mp.start_processes(_pooled_block_worker, args=(2, _free_port(), C, steps, K, out), nprocs=2, join=True,
+                       start_method="spawn")
+    g = np.load(out)
+    _, _, om = make_case("gaussian", 12)
+    st = orc.init(om, PRNGKey(9), C)
+    z, pe, keys = st.z, st.potential_energy, st.rng_key
+    sh = orc.pooled_init_shared(om.d)
+    for _ in range(steps // K):
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
+        orc.pooled_update(om, sums, sh, k_steps=K)
+    assert int(g["i"][0]) == steps
+    np.testing.assert_allclose(g["mu"], sh["mu"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(g["L"], sh["L"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(g["z"], z, rtol=1e-4, atol=1e-4)
+
+
+def test_sync_every_argument_checks():
+    from kernels import PooledARWMH
+    import posteriors as P
+    with pytest.raises(ValueError):
+        PooledARWMH(potential_fn=P.correlated_gaussian(4), num_chains=8, sync_every=0)
+    k = PooledARWMH(potential_fn=P.correlated_gaussian(4), num_chains=8, sync_every=4)
+    with pytest.raises(ValueError):
+        k.init(np.array([0, 1], np.uint32), 6, None, (), {})

@@ -111,20 +111,22 @@ def main():
             print(json.dumps({"config": f"{K.__name__}.sample_Pnx eight schools", "chains": 50000 * 1000, "dim": 10,
                               "steps": 1, "value": reps * 5e7 / wall, "unit": "chain-steps/s",
                               "ms_per_call": wall / reps * 1e3}), flush=True)
-    for key, d, C, kappa in (("gauss256_pooled", 256, 32768, 4.0), ("pooled64", 64, 65536, 2.0)):
-        if key not in want:
+    for key, d, C, kappa, K in (("gauss256_pooled", 256, 32768, 4.0, 1), ("pooled64", 64, 65536, 2.0, 1),
+                                ("gauss256_pooled_k16", 256, 32768, 4.0, 16), ("pooled64_k16", 64, 65536, 2.0, 16)):
+        if key.replace("_k16", "") not in want:
             continue
         g = P.correlated_gaussian(d, log10_kappa=kappa)
-        k = PooledARWMH(potential_fn=g, num_chains=C, device=dev)
+        k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, sync_every=K)
         gen = torch.Generator(device=dev)
         gen.manual_seed(9)
         z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
         st = k.init(PRNGKey(0), 0, z0, (), {})
-        k.sample_(st, args.warmup)
-        wall, kms = timed(lambda: k.sample_(st, 1), args.steps, torch.cuda.current_stream(dev))
-        print(json.dumps({"config": f"{key} regime B", "chains": C, "dim": d, "steps": args.steps,
-                          "value": C * args.steps / wall, "unit": "chain-steps/s", "ms_per_step": kms,
-                          "mean_accept_prob": float(st.mean_accept_prob[0])}), flush=True)
+        k.sample_(st, -(-args.warmup // K) * K)
+        nb = -(-args.steps // K)  # timed blocks of K transitions
+        wall, kms = timed(lambda: k.sample_(st, K), nb, torch.cuda.current_stream(dev))
+        print(json.dumps({"config": f"{key} regime B" + (f", sync_every={K}" if K > 1 else ""), "chains": C,
+                          "dim": d, "steps": nb * K, "value": C * nb * K / wall, "unit": "chain-steps/s",
+                          "ms_per_step": kms / K, "mean_accept_prob": float(st.mean_accept_prob[0])}), flush=True)
 
 
 if __name__ == "__main__":
