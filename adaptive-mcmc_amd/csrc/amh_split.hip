@@ -45,23 +45,35 @@ __global__ __launch_bounds__(kBlock) void propose_kernel(StepParams p, float* __
     const int64_t chain = item_chain<G>(item);
     const bool chain_ok = chain < C;
     const int64_t cl = chain_ok ? chain : C - 1;
-    const float* Lc = p.in.scale + cl * P;
-    const float dl = act ? Lc[col_off(d, r)] : 0.0f;
-    const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+    // The item's factors through one buffer descriptor (wave-uniform base,
+    // range = the item's chains): every column load is unconditional, lanes
+    // above the diagonal and chains past C read 0 out of range, so all the
+    // loads are in flight together (per-lane conditional loads were issued
+    // one round trip at a time).
+    const int64_t first = item * Geo<G>::CPW;
+    const int64_t nvalid = (C - first) < Geo<G>::CPW ? (C - first) : Geo<G>::CPW;
+    const Buf Lb(uniform_ptr(p.in.scale + first * P), (uint32_t)(nvalid * P) * 4u);
+    const int g = lane_id() / G;
+    const uint32_t vrow = act ? ((uint32_t)g * (uint32_t)P + (uint32_t)r) * 4u : kOOB;
+    const float dl = Lb.ld(act ? ((uint32_t)g * (uint32_t)P + (uint32_t)col_off(d, r)) * 4u : kOOB, 0);
     float U[G];
     static_for<G>([&](auto J) {
       constexpr int j = J;
-      U[j] = 0.0f;
-      if (j < d) {
-        const float x = (act && r > j) ? Lc[col_off(d, j) + (r - j)] : 0.0f;
-        const float ij = Gp::template bcast<j>(inv);
-        U[j] = (r == j) ? 1.0f : ((r > j) ? x * ij : 0.0f);
-      }
+      U[j] = (j < d) ? Lb.ld(off_from<G, j>(vrow, kOOB, r), (uint32_t)(col_off(d, j) - j) * 4u) : 0.0f;
     });
     const int32_t it = p.in.i[cl];
     const uint32_t k0 = p.in.rng_key[2 * cl], k1 = p.in.rng_key[2 * cl + 1];
-    const float z = act ? p.in.z[cl * d + r] : 0.0f;
+    const float zr = p.in.z[cl * d + (act ? r : 0)];
+    const float z = act ? zr : 0.0f;
     const float lam = p.in.log_step_size[cl];
+    const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+    static_for<G>([&](auto J) {
+      constexpr int j = J;
+      if (j < d) {
+        const float ij = Gp::template bcast<j>(inv);
+        U[j] = (r == j) ? 1.0f : ((r > j) ? U[j] * ij : 0.0f);
+      }
+    });
     const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
     const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
     const float el = amh_expf(lam);
@@ -94,46 +106,48 @@ typedef __attribute__((address_space(4))) const float cfloat;
 // z = [Intercept, b (Kc), log sigma]; data = [Xc (N x Kc) | Y (N)].  KC > 0:
 // compile-time Kc (the reference data set: K = 25); KC == 0: any Kc <= 30.
 //
-// A block of 4 waves serves 64 chains (lane l = chain 64 * block + l).  The
-// 32 partial sums of the bit spec are independent FMA chains (rows n = r mod
-// 32, each in row order), so wave w owns residues r in [8w, 8w + 8) and reads
-// only those rows: 4x the waves per chain (the scalar-load latency of one
-// row is hidden by the other waves of the SIMD) at unchanged bits.  The 32
-// partials then meet in LDS and wave 0 finishes the chain.
+// A block of 4 waves serves 128 chains: lane l holds chains 128 * block + l
+// and + 64 side by side, so one v_pk_fma_f32 with the row's Xc entry as a
+// broadcast scalar operand (op_sel) advances both chains' fmaf chains, and
+// every scalar load of the data feeds 128 chains.  The 32 partial sums of
+// the bit spec are independent FMA chains (rows n = r mod 32, each in row
+// order), so wave w owns residues r in [8w, 8w + 8) and reads only those
+// rows (the scalar-load latency of one row is hidden by the other waves of
+// the SIMD) at unchanged bits.  The partials then meet in LDS, and waves 0
+// and 1 finish the block's first and second 64 chains.
 constexpr int kDiaWaves = 4;
 constexpr int kDiaRes = 32 / kDiaWaves;  // residues per wave
 
 template <int KC>
 __global__ __launch_bounds__(64 * kDiaWaves) void diamonds_pot_lane_kernel(PotParams p) {
   constexpr int KMAX = KC > 0 ? KC : 30;
-  __shared__ float pl[32][64];
+  __shared__ float pl[32][128];
   const int Kc = KC > 0 ? KC : (int)p.model.k - 1;
   const int d = p.d;
   const int64_t N = p.model.n;
   const int64_t n_ch = p.n;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
-  int64_t c = (int64_t)blockIdx.x * 64 + lane;
-  const bool ok = c < n_ch;
-  if (!ok) c = n_ch - 1;
-  const float* zc = p.z + c * d;
-  float b[KMAX];
-  static_for<KMAX>([&](auto K) { b[K] = (K < Kc) ? zc[1 + K] : 0.0f; });
-  const float icpt = zc[0];
-  const float ls = zc[Kc + 1];
-  const float sg = amh_expf(ls);
-  const float isg = 1.0f / sg;
+  const int64_t c0 = (int64_t)blockIdx.x * 128 + lane;
+  const float* z0 = p.z + (c0 < n_ch ? c0 : n_ch - 1) * d;
+  const float* z1 = p.z + (c0 + 64 < n_ch ? c0 + 64 : n_ch - 1) * d;
+  f32x2v b2[KMAX];
+  static_for<KMAX>([&](auto K) { b2[K] = (K < Kc) ? f32x2v{z0[1 + K], z1[1 + K]} : f32x2v{0.0f, 0.0f}; });
+  const f32x2v icpt2 = {z0[0], z1[0]};
+  const f32x2v ls2 = {z0[Kc + 1], z1[Kc + 1]};
+  const f32x2v sg2 = {amh_expf(ls2[0]), amh_expf(ls2[1])};
+  const f32x2v isg2 = {1.0f / sg2[0], 1.0f / sg2[1]};
   const cfloat* X = (const cfloat*)p.model.data;
   const cfloat* Y = X + N * Kc;
-  float part[kDiaRes];
-  static_for<kDiaRes>([&](auto Q) { part[Q] = 0.0f; });
-  auto row = [&](const float (&xr)[KMAX], float yn, float& acc) {
-    float mu = 0.0f;
+  f32x2v part2[kDiaRes];
+  static_for<kDiaRes>([&](auto Q) { part2[Q] = f32x2v{0.0f, 0.0f}; });
+  auto row = [&](const float (&xr)[KMAX], float yn, f32x2v& acc) {
+    f32x2v mu = {0.0f, 0.0f};
     static_for<KMAX>([&](auto K) {
-      if (K < Kc) mu = fmaf(xr[K], b[K], mu);
+      if (K < Kc) mu = __builtin_elementwise_fma(f32x2v{xr[K], xr[K]}, b2[K], mu);
     });
-    const float e = (yn - (icpt + mu)) * isg;
-    acc = fmaf(e, e, acc);
+    const f32x2v e = (f32x2v{yn, yn} - (icpt2 + mu)) * isg2;
+    acc = __builtin_elementwise_fma(e, e, acc);
   };
   auto load = [&](int64_t n, float (&xr)[KMAX], float& yn) {
     static_for<KMAX>([&](auto K) { xr[K] = (K < Kc) ? X[n * Kc + K] : 0.0f; });
@@ -156,7 +170,7 @@ __global__ __launch_bounds__(64 * kDiaWaves) void diamonds_pot_lane_kernel(PotPa
           nn = (m + 1 < Mfull) ? 32 * (m + 1) + r0 : 32 * m + r0 + Q;
         }
         load(nn, nxt, ynxt);
-        row(cur, ycur, part[Q]);
+        row(cur, ycur, part2[Q]);
         static_for<KMAX>([&](auto K) { cur[K] = nxt[K]; });
         ycur = ynxt;
       });
@@ -167,31 +181,40 @@ __global__ __launch_bounds__(64 * kDiaWaves) void diamonds_pot_lane_kernel(PotPa
     if (n < N) {
       float xr[KMAX], yn;
       load(n, xr, yn);
-      row(xr, yn, part[Q]);
+      row(xr, yn, part2[Q]);
     }
   });
-  static_for<kDiaRes>([&](auto Q) { pl[r0 + Q][lane] = part[Q]; });
+  static_for<kDiaRes>([&](auto Q) {
+    pl[r0 + Q][lane] = part2[Q][0];
+    pl[r0 + Q][64 + lane] = part2[Q][1];
+  });
   __syncthreads();
-  if (w != 0) return;
+  if (w >= 2) return;
+  const int h = w;  // this wave finishes chain c0 + 64 h
+  const int64_t c = c0 + 64 * h;
   float all[32];
-  static_for<32>([&](auto R) { all[R] = pl[R][lane]; });
+  static_for<32>([&](auto R) { all[R] = pl[R][64 * h + lane]; });
   const float S = butterfly32(all);
   float bb[32];  // group lane r holds coordinate r: b_{r-1}^2 for 1 <= r <= Kc
   static_for<32>([&](auto R) {
     constexpr int r = R;
     if constexpr (r >= 1 && r - 1 < KMAX) {
-      bb[r] = (r <= Kc) ? b[r - 1] * b[r - 1] : 0.0f;
+      const float br = h ? b2[r - 1][1] : b2[r - 1][0];
+      bb[r] = (r <= Kc) ? br * br : 0.0f;
     } else {
       bb[r] = 0.0f;
     }
   });
   const float B = butterfly32(bb);
+  const float icpt = h ? icpt2[1] : icpt2[0];
+  const float ls = h ? ls2[1] : ls2[0];
+  const float sg = h ? sg2[1] : sg2[0];
   const float cst = -3.30347394261755545f;
   const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
   const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
   const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
   const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
-  if (ok) p.pe[c] = -(((ll + lpb) + lpi) + lps);
+  if (c < n_ch) p.pe[c] = -(((ll + lpb) + lpi) + lps);
 }
 
 // ---------------------------------------------------------------- launchers --
@@ -206,7 +229,7 @@ hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
 
 hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s) {
   if (!split_model(model_id, p.d)) return hipErrorInvalidValue;
-  const int64_t blocks = (p.n + 63) / 64;
+  const int64_t blocks = (p.n + 127) / 128;
   if (p.model.k - 1 == 24) {
     hipLaunchKernelGGL(diamonds_pot_lane_kernel<24>, dim3((unsigned)blocks), dim3(64 * kDiaWaves), 0, s, p);
   } else {

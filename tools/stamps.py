@@ -25,11 +25,17 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--chains", type=int, default=65536)
 ap.add_argument("--dim", type=int, default=64)
 ap.add_argument("--steps", type=int, default=1)
+ap.add_argument("--model", default="gaussian", help="gaussian | diamonds (split path: the ExtPotM step kernel)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 C, d = a.chains, a.dim
-k = ARWMH(potential_fn=P.correlated_gaussian(d), num_chains=C, device=dev)
-st = k.init(PRNGKey(0), 0, (torch.rand(C, d, device=dev) * 4 - 2).contiguous(), (), {})
+if a.model == "diamonds":
+    mk = P.synthetic_diamonds()
+    k = ARWMH(model=P.diamonds, num_chains=C, device=dev)
+    st = k.init(PRNGKey(0), 0, None, (), mk)
+else:
+    k = ARWMH(potential_fn=P.correlated_gaussian(d), num_chains=C, device=dev)
+    st = k.init(PRNGKey(0), 0, (torch.rand(C, d, device=dev) * 4 - 2).contiguous(), (), {})
 for _ in range(20):
     k.sample_(st, a.steps)
 torch.cuda.synchronize()
