@@ -159,6 +159,9 @@ hipError_t run_big_potential(const PotParams& p, hipStream_t s);
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain
 // batched potential, then the step kernel reading U(z') (amh_split.hip)
 bool split_model(int model_id, int d);
+// the reference diamonds data (K = 25 columns): d = 26, compiled as a fixed
+// dimension on the split path
+constexpr int kDiamondsD = 26;
 hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s);
 hipError_t run_step_ext(const StepParams& p, hipStream_t s);
 hipError_t run_init_nopot(const InitParams& p, hipStream_t s);

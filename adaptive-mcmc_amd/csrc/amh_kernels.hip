@@ -161,14 +161,16 @@ __host__ __device__ __forceinline__ size_t step_lds_bytes(const ModelArgs& m, in
   return (tickets_off<G, M>(m, d) + 4) * sizeof(float);
 }
 
-template <int DMAX, template <int> class M, bool EXACT>
+// DFIX > 0: d fixed at compile time below the group width (the diamonds
+// split path, d = 26 in groups of 32): column offsets become immediates.
+template <int DMAX, template <int> class M, bool EXACT, int DFIX = 0>
 __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   constexpr int G = DMAX;
   constexpr int CPW = Geo<G>::CPW;
   constexpr bool kExt = is_external<M<G>>::value;
   using Gp = Grp<G>;
   extern __shared__ float lds[];
-  const int d = EXACT ? DMAX : p.d;
+  const int d = EXACT ? DMAX : (DFIX > 0 ? DFIX : p.d);
   M<G>::stage(lds, p.model, d);
   if (threadIdx.x == 0) lds[tickets_off<G, M>(p.model, d)] = 0.0f;  // ticket counter (bits 0)
   __syncthreads();
@@ -681,7 +683,7 @@ static int grid_for(int64_t n_items, int waves_per_block) {
   return (int)(blocks < cap ? (blocks > 0 ? blocks : 1) : cap);
 }
 
-template <int DMAX, template <int> class M, bool EXACT>
+template <int DMAX, template <int> class M, bool EXACT, int DFIX = 0>
 hipError_t launch_step(const StepParams& p, hipStream_t s) {
   constexpr int CPW = Geo<DMAX>::CPW;
   constexpr int WPB = kBlockStep / 64;
@@ -689,7 +691,7 @@ hipError_t launch_step(const StepParams& p, hipStream_t s) {
   const int64_t n_items = (p.C + CPW - 1) / CPW;
   const size_t shm = step_lds_bytes<DMAX, M>(p.model, d);
   if (shm > 163840) return hipErrorInvalidConfiguration;
-  auto kern = arwmh_step_kernel<DMAX, M, EXACT>;
+  auto kern = arwmh_step_kernel<DMAX, M, EXACT, DFIX>;
   // persistent grid: as many blocks as are co-resident (each wave then walks
   // chain groups wave, wave + total_waves, ...)
   int per_cu = 0;
@@ -775,6 +777,7 @@ hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s) {
 // and init without the potential (filled by the batched potential kernel)
 hipError_t run_step_ext(const StepParams& p, hipStream_t s) {
   if (p.d < 1 || p.d > 32 || p.n_steps != 1 || p.ext_pe == nullptr) return hipErrorInvalidValue;
+  if (p.d == kDiamondsD) return launch_step<32, ExtPotM, false, kDiamondsD>(p, s);
   return launch_step<32, ExtPotM, false>(p, s);
 }
 hipError_t run_init_nopot(const InitParams& p, hipStream_t s) {

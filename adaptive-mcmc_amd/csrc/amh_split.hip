@@ -30,19 +30,23 @@ bool split_model(int model_id, int d) { return model_id == AMH_MODEL_DIAMONDS &&
 // Lane group of G = 32 per chain, lane r = row r; the factor is read straight
 // from HBM (each column of a chain is one coalesced access).  U_rj and the
 // four partial sums follow arwmh_step_kernel exactly.
-template <int G>
+template <int G, int DFIX = 0>
 __global__ __launch_bounds__(kBlock) void propose_kernel(StepParams p, float* __restrict__ xprop) {
   using Gp = Grp<G>;
-  const int d = p.d;
-  const int r = Gp::r();
-  const bool act = r < d;
+  const int d = DFIX > 0 ? DFIX : p.d;
   const int64_t C = p.C;
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
   const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
   const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
   for (int64_t item = wave0; item < n_items; item += wstride) {
-    const int64_t chain = item_chain<G>(item);
+    // lane-dependent values from an opaque lane id inside the loop, so the
+    // per-column load offsets are not hoisted out of it (VGPR pressure)
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int r = lane & (G - 1);
+    const bool act = r < d;
+    const int64_t chain = item * Geo<G>::CPW + lane / G;
     const bool chain_ok = chain < C;
     const int64_t cl = chain_ok ? chain : C - 1;
     // The item's factors through one buffer descriptor (wave-uniform base,
@@ -53,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void propose_kernel(StepParams p, float* __
     const int64_t first = item * Geo<G>::CPW;
     const int64_t nvalid = (C - first) < Geo<G>::CPW ? (C - first) : Geo<G>::CPW;
     const Buf Lb(uniform_ptr(p.in.scale + first * P), (uint32_t)(nvalid * P) * 4u);
-    const int g = lane_id() / G;
+    const int g = lane / G;
     const uint32_t vrow = act ? ((uint32_t)g * (uint32_t)P + (uint32_t)r) * 4u : kOOB;
     const float dl = Lb.ld(act ? ((uint32_t)g * (uint32_t)P + (uint32_t)col_off(d, r)) * 4u : kOOB, 0);
     float U[G];
@@ -223,7 +227,12 @@ hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
   const int64_t n_items = (p.C + Geo<32>::CPW - 1) / Geo<32>::CPW;
   int64_t blocks = (n_items + kBlock / 64 - 1) / (kBlock / 64);
   if (blocks > 256 * 32) blocks = 256 * 32;
-  hipLaunchKernelGGL(propose_kernel<32>, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s, p, xprop);
+  if (p.d == kDiamondsD) {
+    hipLaunchKernelGGL((propose_kernel<32, kDiamondsD>), dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s,
+                       p, xprop);
+  } else {
+    hipLaunchKernelGGL(propose_kernel<32>, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s, p, xprop);
+  }
   return hipGetLastError();
 }
 
