@@ -21,7 +21,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "arwmh_step_kernel<64, amh::GaussianM, true>"
+KERNEL = "arwmh_step_kernel<64, amh::GaussianM, true"  # prefix: later builds add template args
 
 
 def step_rows(path):
@@ -58,7 +58,7 @@ def main():
     traffic = 2 * fetch_kib * 1024 + write_kib * 1024
     out = {
         "tag": a.tag,
-        "kernel": f"amh::{KERNEL}",
+        "kernel": next(iter(r["Kernel_Name"] for r in tr)),
         "workload": f"bench.py single-step launches, {C} chains, d={d}",
         "launches_timed": len(timed),
         "avg_us": statistics.mean(timed),
