@@ -70,6 +70,13 @@ int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d
       if (n_data != N * (K - 1) + N) { *why = "diamonds data must hold N*(K-1) + N floats"; return -1; }
       return (int)(K + 1);
     }
+    case AMH_MODEL_DIAMONDS_SS: {
+      if (nip < 2) { *why = "diamonds_suffstat needs iparams {N, K}"; return -1; }
+      const int64_t Kc = ip[1] - 1;
+      if (Kc < 1 || Kc > 30) { *why = "diamonds_suffstat needs 2 <= K <= 31"; return -1; }
+      if (n_data != 2 * (4 + 2 * Kc + Kc * Kc)) { *why = "diamonds_suffstat data must hold 2 (4 + 2 Kc + Kc^2) floats"; return -1; }
+      return (int)(Kc + 2);
+    }
     default:
       *why = "unknown model id";
       return -1;
@@ -152,8 +159,9 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
     return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model with d a multiple of 32 (<= 256)");
   h->model_id = model_id;
   h->model.data = data;
-  h->model.n = (model_id == AMH_MODEL_KIDIQ || model_id == AMH_MODEL_DIAMONDS) ? iparams[0] : 0;
-  h->model.k = (model_id == AMH_MODEL_DIAMONDS) ? iparams[1] : 0;
+  const bool dia = model_id == AMH_MODEL_DIAMONDS || model_id == AMH_MODEL_DIAMONDS_SS;
+  h->model.n = (model_id == AMH_MODEL_KIDIQ || dia) ? iparams[0] : 0;
+  h->model.k = dia ? iparams[1] : 0;
   h->n_data = n_data;
   return AMH_OK;
 }

@@ -448,6 +448,112 @@ struct DiamondsM {
   }
 };
 
+// Diamonds through sufficient statistics (AMH_MODEL_DIAMONDS_SS).  The
+// likelihood's residual sum is an exact quadratic in (Intercept, b):
+//   sum_n (Y_n - I - Xc_n b)^2 = A + a (N a - 2 sT) - 2 b'(t - a sx) + b'Gm b,
+// a = I - ybar, T = Y - ybar, A = T'T, sT = sum T, t = Xc'T, sx = sum Xc_n,
+// Gm = Xc'Xc, all float64 statistics of the same float32 Xc and Y the direct
+// model reads (posteriors.diamonds_suffstat).  Per chain-step this is
+// O(Kc^2) float64 work instead of the N*Kc float32 contraction, so the model
+// runs inside the one-launch step kernel with the factor read once.  Only the
+// residual sum differs from DiamondsM (float64, then rounded); priors and
+// the rest of U are the same float ops.
+// data = float64 [N, ybar, A, sT, t (Kc), sx (Kc), Gm (Kc x Kc, row-major)]
+// passed as pairs of floats.  Everything lives in LDS (float64), so a lane
+// keeps no model registers between chain groups:
+//   row i (i < Kc) at i * ldr: [Gm_i0 .. Gm_i,i-1, 0 .. 0 (to Kc), Gm_ii, t_i, sx_i, pad]
+//   header at Kc * ldr:        [N, ybar, A, sT]
+template <int G>
+struct DiamondsSSM {
+  struct Ctx {};
+  static __host__ __device__ int ldr(int Kc) { return (Kc + 4) & ~1; }  // doubles per row (16-B rows)
+  static __host__ __device__ size_t lds_bytes(const ModelArgs&, int d) {
+    return (size_t)((d - 2) * ldr(d - 2) + 4) * sizeof(double);
+  }
+  static __device__ void stage(float* lds, const ModelArgs& m, int d) {
+    const int Kc = d - 2, L = ldr(Kc);
+    const double* D = (const double*)m.data;
+    const double* Gm = D + 4 + 2 * Kc;
+    double* out = (double*)lds;
+    for (int k = threadIdx.x; k < Kc * L + 4; k += blockDim.x) {
+      const int i = k / L, j = k - i * L;
+      double v = 0.0;
+      if (i >= Kc) v = D[j];                         // header
+      else if (j < i) v = Gm[i * Kc + j];
+      else if (j == Kc) v = Gm[i * Kc + i];
+      else if (j == Kc + 1) v = D[4 + i];            // t_i
+      else if (j == Kc + 2) v = D[4 + Kc + i];       // sx_i
+      out[k] = v;
+    }
+  }
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs&, int, int) { return Ctx{}; }
+  static __device__ __forceinline__ double lo(const f32x4& q) { return __builtin_bit_cast(double, f32x2v{q[0], q[1]}); }
+  static __device__ __forceinline__ double hi(const f32x4& q) { return __builtin_bit_cast(double, f32x2v{q[2], q[3]}); }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx&, const float* lds) {
+    const int Kc = d - 2;
+    const int L = ldr(Kc);
+    const float icpt = Grp<G>::template bcast<0>(x);
+    const float ls = Grp<G>::bcast_rt(x, Kc + 1);
+    const float sg = amh_expf(ls);
+    const float isg = 1.0f / sg;
+    const bool act = r >= 1 && r <= Kc;
+    const uint32_t prow = lds_addr(lds + 2 * (act ? r - 1 : 0) * L);
+    const uint32_t phdr = lds_addr(lds + 2 * Kc * L);
+    // rr = sum_{j < i} Gm_ij b_j in j order (the row's zeros at j >= i add +0)
+    double rr = 0.0;
+    static_for<(G + 3) / 4>([&](auto B) {  // 4 columns (two ds_read_b128) per wait
+      constexpr int b = B;
+      if (4 * b < Kc) {
+        f32x4 p0 = lds_ld4<32 * b>(prow);
+        f32x4 p1 = (4 * b + 2 < Kc) ? lds_ld4<32 * b + 16>(prow) : f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(p0), "+v"(p1));
+        static_for<4>([&](auto K) {
+          constexpr int j = 4 * b + K;
+          if constexpr (j + 1 < G) {
+            if (j < Kc) {
+              const f32x4& q = (K < 2) ? p0 : p1;
+              const double g = (K % 2 == 0) ? lo(q) : hi(q);
+              rr = __builtin_fma(act ? g : 0.0, (double)Grp<G>::template bcast<1 + j>(x), rr);
+            }
+          }
+        });
+      }
+    });
+    // Gm_ii, t_i, sx_i at columns Kc .. Kc+2 of the row; header N, ybar, A, sT
+    const uint32_t pdiag = prow + 8u * (uint32_t)Kc;  // Kc even or odd: 8-B aligned reads
+    f32x2v g2, t2, s2;
+    asm volatile("ds_read_b64 %0, %1 offset:0" : "=v"(g2) : "v"(pdiag));
+    asm volatile("ds_read_b64 %0, %1 offset:8" : "=v"(t2) : "v"(pdiag));
+    asm volatile("ds_read_b64 %0, %1 offset:16" : "=v"(s2) : "v"(pdiag));
+    f32x4 h0 = lds_ld4<0>(phdr), h1 = lds_ld4<16>(phdr);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(g2), "+v"(t2), "+v"(s2), "+v"(h0), "+v"(h1));
+    const double gii = __builtin_bit_cast(double, g2), ti = __builtin_bit_cast(double, t2);
+    const double sxi = __builtin_bit_cast(double, s2);
+    const double N = lo(h0), ybar = hi(h0), A = lo(h1), sT = hi(h1);
+    const double a = (double)icpt - ybar;
+    const double bi = act ? (double)x : 0.0;
+    const double quad = bi * __builtin_fma(2.0, rr, gii * bi);
+    const double lin = bi * __builtin_fma(-a, sxi, ti);
+    double v = act ? __builtin_fma(-2.0, lin, quad) : 0.0;
+    static_for<5>([&](auto S) {  // xor butterfly over the group (oracle dgroup_sum)
+      constexpr int off = 1 << S;
+      if constexpr (off < G) v = v + __shfl_xor(v, off, G);
+    });
+    const double qa = __builtin_fma(a, __builtin_fma(N, a, -2.0 * sT), A);
+    const double q = qa + v;
+    const double isgd = (double)isg;
+    const float S = (float)(q * (isgd * isgd));
+    const float bb = act ? x * x : 0.0f;
+    const float B = Grp<G>::sum(bb);
+    const float cst = -3.30347394261755545f;
+    const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+    const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+    const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+    return -(((ll + lpb) + lpi) + lps);
+  }
+};
+
 // Potential evaluated outside the step kernel (split path, amh_split.hip):
 // the step kernel reads U(z') from StepParams::ext_pe instead of calling
 // potential(); init leaves pe for the batched potential kernel to fill.
@@ -590,6 +696,9 @@ static hipError_t dispatch(int model_id, int d, F&& f) {
     case AMH_MODEL_DIAMONDS:
       if (d > 32) return hipErrorInvalidValue;
       return f.template operator()<32, DiamondsM, false>();
+    case AMH_MODEL_DIAMONDS_SS:
+      if (d < 3 || d > 32) return hipErrorInvalidValue;
+      return f.template operator()<32, DiamondsSSM, false>();
     default:
       return hipErrorInvalidValue;
   }

@@ -762,6 +762,8 @@ struct PnxF {
 };
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
+  // diamonds at the reference shape: compile-time d (immediate offsets)
+  if (model_id == AMH_MODEL_DIAMONDS_SS && p.d == kDiamondsD) return launch_step<32, DiamondsSSM, false, kDiamondsD>(p, s);
   return dispatch(model_id, p.d, StepF{p, s});
 }
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s) {

@@ -436,6 +436,9 @@ hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* su
       return f.template operator()<64, KidiqM, false>();
     case AMH_MODEL_DIAMONDS:
       return f.template operator()<64, DiamondsM, false>();
+    case AMH_MODEL_DIAMONDS_SS:
+      if (d < 3 || d > 32) return hipErrorInvalidValue;
+      return f.template operator()<64, DiamondsSSM, false>();
     default:
       return hipErrorInvalidValue;
   }

@@ -20,6 +20,7 @@ AMH_MODEL_GAUSSIAN = 1
 AMH_MODEL_EIGHT_SCHOOLS = 2
 AMH_MODEL_KIDIQ = 3
 AMH_MODEL_DIAMONDS = 4
+AMH_MODEL_DIAMONDS_SS = 5
 
 # every symbol include/amh.h declares
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",

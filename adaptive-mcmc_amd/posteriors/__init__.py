@@ -144,6 +144,34 @@ def _dia_pack(data):
 diamonds = Model("diamonds", _lib.AMH_MODEL_DIAMONDS, _dia_sites, _dia_pack, None,
                  "Intercept ~ t3(8,10), b ~ N(0,1), sigma ~ |t3(0,10)|, Y ~ N(Intercept + Xc b, sigma)")
 
+
+def diamonds_suffstats(data) -> np.ndarray:
+    """float64 statistics of the float32 centred design the direct model reads
+    (_dia_pack): [N, ybar, A = T'T, sT = sum T, t = Xc'T (Kc), sx = sum_n Xc_n
+    (Kc), Gm = Xc'Xc (Kc x Kc, row-major)], T = Y - ybar."""
+    flat, (N, K) = _dia_pack(data)
+    Kc = K - 1
+    Xc = flat[:N * Kc].reshape(N, Kc).astype(np.float64)
+    Y = flat[N * Kc:].astype(np.float64)
+    ybar = Y.mean()
+    T = Y - ybar
+    head = np.array([N, ybar, T @ T, T.sum()])
+    return np.concatenate([head, Xc.T @ T, Xc.sum(axis=0), (Xc.T @ Xc).reshape(-1)])
+
+
+def _dia_ss_pack(data):
+    st = np.ascontiguousarray(diamonds_suffstats(data), dtype=np.float64)
+    N, K = _np(data["X"]).shape
+    return st.view(np.float32), (N, K)
+
+
+# The same posterior with the likelihood's residual sum taken from float64
+# sufficient statistics (O(K^2) per evaluation instead of O(N K)); it runs in
+# the one-launch step kernel.  U differs from `diamonds` by the rounding of
+# the float32 residual sum only (DESIGN.md §3.7).
+diamonds_suffstat = Model("diamonds_suffstat", _lib.AMH_MODEL_DIAMONDS_SS, _dia_sites, _dia_ss_pack, None,
+                          "diamonds, residual sum from float64 sufficient statistics")
+
 # mean of the stored PosteriorDB reference draws for b[:4], Intercept, sigma
 # (python/mcmc_runs/diamonds-example-references.pkl, read byte-wise; SURVEY.md §8(c).7)
 _DIAMONDS_B_HEAD = np.array([6.660, 6.363, -4.684, 1.447])
@@ -229,4 +257,5 @@ REGISTRY = {
     "kidiq": kidiq,
     "kidiq_kidscore_momhsiq": kidiq,
     "diamonds": diamonds,
+    "diamonds_suffstat": diamonds_suffstat,
 }

@@ -31,7 +31,7 @@
 
 #define ORC_DMAX 64
 
-enum { ORC_GAUSSIAN = 1, ORC_EIGHT_SCHOOLS = 2, ORC_KIDIQ = 3, ORC_DIAMONDS = 4 };
+enum { ORC_GAUSSIAN = 1, ORC_EIGHT_SCHOOLS = 2, ORC_KIDIQ = 3, ORC_DIAMONDS = 4, ORC_DIAMONDS_SS = 5 };
 
 typedef struct {
   int32_t model_id;
@@ -55,7 +55,7 @@ int orc_group_width(int d) {
 /* Group width of the per-chain kernels for a model (amh_device.h dispatch):
  * eight schools runs at G = 16 and diamonds at G = 32 for every d they take. */
 static int orc_gw(const orc_cfg* cfg) {
-  if (cfg->model_id == ORC_DIAMONDS) return 32;
+  if (cfg->model_id == ORC_DIAMONDS || cfg->model_id == ORC_DIAMONDS_SS) return 32;
   if (cfg->model_id == ORC_EIGHT_SCHOOLS) return 16;
   return orc_group_width(cfg->d);
 }
@@ -224,6 +224,62 @@ static float pot_diamonds(const orc_cfg* cfg, const float* x, int G) {
   return -(((ll + lpb) + lpi) + lps);
 }
 
+/* diamonds through float64 sufficient statistics (amh_device.h DiamondsSSM;
+ * model run_diamonds_lr_decay.py:24-40 as pot_diamonds).  data = float64
+ * [N, ybar, A, sT, t (Kc), sx (Kc), Gm (Kc x Kc)]; the residual sum is
+ * A + a (N a - 2 sT) + sum_i [b_i (2 rr_i + Gm_ii b_i) - 2 b_i (t_i - a sx_i)]
+ * with rr_i = sum_{j<i} Gm_ij b_j, the per-coordinate terms summed by the
+ * group butterfly in float64. */
+static double dgroup_sum(const double* in, int G) {
+  double x[ORC_DMAX], y[ORC_DMAX];
+  memcpy(x, in, sizeof(double) * G);
+  for (int off = 1; off < G; off <<= 1) {
+    for (int r = 0; r < G; ++r) y[r] = x[r] + x[r ^ off];
+    memcpy(x, y, sizeof(double) * G);
+  }
+  return x[0];
+}
+
+static float pot_diamonds_ss(const orc_cfg* cfg, const float* x, int G) {
+  const int Kc = cfg->d - 2;
+  const double* D = (const double*)cfg->data;
+  const double N = D[0], ybar = D[1], A = D[2], sT = D[3];
+  const double* t = D + 4;
+  const double* sx = D + 4 + Kc;
+  const double* Gm = D + 4 + 2 * Kc;
+  const float icpt = x[0], ls = x[Kc + 1];
+  const float sg = amh_expf(ls);
+  const float isg = 1.0f / sg;
+  const double a = (double)icpt - ybar;
+  double v[ORC_DMAX];
+  float bb[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    v[r] = 0.0;
+    bb[r] = 0.0f;
+    if (r < 1 || r > Kc) continue;
+    const int i = r - 1;
+    const double bi = (double)x[r];
+    double rr = 0.0;
+    for (int j = 0; j < Kc; ++j) rr = fma(j < i ? Gm[i * Kc + j] : 0.0, (double)x[1 + j], rr);
+    const double quad = bi * fma(2.0, rr, Gm[i * Kc + i] * bi);
+    const double lin = bi * fma(-a, sx[i], t[i]);
+    v[r] = fma(-2.0, lin, quad);
+    bb[r] = x[r] * x[r];
+  }
+  const double Q = dgroup_sum(v, G);
+  const double qa = fma(a, fma(N, a, -2.0 * sT), A);
+  const double q = qa + Q;
+  const double isgd = (double)isg;
+  const float S = (float)(q * (isgd * isgd));
+  const float B = group_sum(bb, G);
+  const float cst = -3.30347394261755545f;
+  const float ll = fmaf(-0.5f, S, (float)N * ((-ls) - HALF_LOG_2PI));
+  const float lpb = fmaf(-0.5f, B, -(float)Kc * HALF_LOG_2PI);
+  const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+  const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+  return -(((ll + lpb) + lpi) + lps);
+}
+
 static float pot_gaussian_big(const orc_cfg* cfg, const float* x);
 
 float orc_potential1(const orc_cfg* cfg, const float* x) {
@@ -234,6 +290,7 @@ float orc_potential1(const orc_cfg* cfg, const float* x) {
     case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
     case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
     case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
+    case ORC_DIAMONDS_SS: return pot_diamonds_ss(cfg, x, G);
     default: return NAN;
   }
 }
@@ -613,6 +670,7 @@ static float orc_potential_g(const orc_cfg* cfg, const float* x, int G) {
     case ORC_EIGHT_SCHOOLS: return pot_eight_schools(cfg, x, G);
     case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
     case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
+    case ORC_DIAMONDS_SS: return pot_diamonds_ss(cfg, x, G);
     default: return NAN;
   }
 }

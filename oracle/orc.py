@@ -19,7 +19,7 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "libamh_oracle.so")
 
-GAUSSIAN, EIGHT_SCHOOLS, KIDIQ, DIAMONDS = 1, 2, 3, 4
+GAUSSIAN, EIGHT_SCHOOLS, KIDIQ, DIAMONDS, DIAMONDS_SS = 1, 2, 3, 4, 5
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

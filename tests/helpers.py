@@ -26,6 +26,11 @@ def make_case(kind: str, d: int = None):
         arr, ip = P.diamonds.pack_fn(mk)
         N, K = ip
         return dict(model=P.diamonds), mk, orc.Model(orc.DIAMONDS, K + 1, arr, n_data=N, k_data=K)
+    if kind == "diamonds_ss":
+        mk = P.synthetic_diamonds(N=500)
+        arr, ip = P.diamonds_suffstat.pack_fn(mk)
+        N, K = ip
+        return dict(model=P.diamonds_suffstat), mk, orc.Model(orc.DIAMONDS_SS, K + 1, arr, n_data=N, k_data=K)
     raise ValueError(kind)
 
 

@@ -26,14 +26,14 @@ def _init(kind, C, gpu, orc, seed=0, d=None, num_warmup=0):
     return k, st, om, ost
 
 
-@pytest.mark.parametrize("kind", ["gaussian", "eight_schools", "kidiq", "diamonds"])
+@pytest.mark.parametrize("kind", ["gaussian", "eight_schools", "kidiq", "diamonds", "diamonds_ss"])
 def test_init_bitexact(kind, gpu, orc):
     k, st, om, ost = _init(kind, 333, gpu, orc)
     assert_state_bitequal(st, ost, f"{kind} init")
 
 
 @pytest.mark.parametrize("kind,d", [("gaussian", 64), ("gaussian", 5), ("gaussian", 16), ("gaussian", 33),
-                                    ("eight_schools", None), ("kidiq", None), ("diamonds", None),
+                                    ("eight_schools", None), ("kidiq", None), ("diamonds", None), ("diamonds_ss", None),
                                     ("gaussian", 96), ("gaussian", 256)])
 def test_potential_bitexact(kind, d, gpu, orc):
     k, st, om, ost = _init(kind, 8, gpu, orc, d=d)
@@ -45,7 +45,7 @@ def test_potential_bitexact(kind, d, gpu, orc):
 
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("gaussian", 7, 517), ("gaussian", 32, 300),
                                       ("eight_schools", None, 400), ("kidiq", None, 257),
-                                      ("diamonds", None, 66)])
+                                      ("diamonds", None, 66), ("diamonds_ss", None, 333)])
 def test_single_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.sample (one launch per step) vs oracle step(n_steps=1), 40 steps."""
     k, st, om, ost = _init(kind, C, gpu, orc, d=d, num_warmup=10)
@@ -59,7 +59,7 @@ def test_single_steps_bitexact(kind, d, C, gpu, orc):
 
 
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 2000), ("eight_schools", None, 1000),
-                                      ("diamonds", None, 130)])
+                                      ("diamonds", None, 130), ("diamonds_ss", None, 1000)])
 def test_fused_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.run (n steps in one launch, z collected) vs oracle step(n_steps)."""
     k, st, om, ost = _init(kind, C, gpu, orc, d=d)
@@ -244,3 +244,26 @@ def test_gpu_follows_golden(name, gpu):
             np.testing.assert_allclose(st.z.cpu().numpy(), f["z"][j], rtol=tl["z"][0], atol=tl["z"][1])
             np.testing.assert_allclose(st.adapt_state.loc.cpu().numpy(), f["loc"][j], rtol=tl["loc"][0],
                                        atol=tl["loc"][1])
+
+
+def test_diamonds_suffstat_generic_k(gpu, orc):
+    """Sufficient-statistics diamonds off the reference shape (K = 10, N = 77,
+    d = 11 in the G = 32 group): init, thinned collection and the potential
+    bit-identical to the oracle."""
+    import posteriors as P
+    from kernels import ARWMH, PRNGKey
+    mk = P.synthetic_diamonds(N=77, K=10, seed=5)
+    arr, (N, K) = P.diamonds_suffstat.pack_fn(mk)
+    om = orc.Model(orc.DIAMONDS_SS, K + 1, arr, n_data=N, k_data=K)
+    C = 199
+    k = ARWMH(model=P.diamonds_suffstat, num_chains=C)
+    st = k.init(PRNGKey(4), 5, None, (), mk)
+    ost = orc.init(om, PRNGKey(4), C)
+    assert_state_bitequal(st, ost, "suffstat init")
+    st2, cz, cp = k.run(st, 12, thinning=4, collect_z=True, collect_pe=True)
+    ocz = orc.step(om, ost, 12, num_warmup=5, collect_z=True)
+    np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), ocz[3::4].view(np.uint32))
+    assert_state_bitequal(st2, ost, "suffstat run")
+    z = np.random.default_rng(2).normal(size=(300, K + 1)).astype(np.float32)
+    pe = k.potential(torch.as_tensor(z, device=gpu)).cpu().numpy()
+    np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))

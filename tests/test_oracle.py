@@ -32,6 +32,11 @@ def lit_potential(kind, om):
     if kind == "diamonds":
         N, Kc = om.n_data, om.k_data - 1
         return lambda z: lit.diamonds_potential(z, data[:N * Kc].reshape(N, Kc), data[N * Kc:])
+    if kind == "diamonds_ss":  # same posterior: the literal model reads the direct data
+        import posteriors as P
+        arr, (N, K) = P.diamonds.pack_fn(P.synthetic_diamonds(N=500))
+        arr = arr.astype(np.float64)
+        return lambda z: lit.diamonds_potential(z, arr[:N * (K - 1)].reshape(N, K - 1), arr[N * (K - 1):])
     raise ValueError(kind)
 
 
@@ -79,7 +84,8 @@ def test_nan_potential_rejects():
 
 # ------------------------------------------------- C oracle vs literal numpy --
 @pytest.mark.parametrize("kind,dim", [("gaussian", 12), ("eight_schools", None), ("kidiq", None),
-                                      ("diamonds", None), ("gaussian", 128), ("gaussian", 256)])
+                                      ("diamonds", None), ("diamonds_ss", None), ("gaussian", 128),
+                                      ("gaussian", 256)])
 @pytest.mark.parametrize("pre_steps", [0, 1, 37])
 def test_oracle_step_matches_literal(kind, dim, pre_steps, orc):
     """One teacher-forced transition (identical noise) of the C oracle against
@@ -169,3 +175,33 @@ def test_eight_schools_posterior(orc):
     assert abs(mu.mean() - 4.40) < 0.35 and abs(mu.std() - 3.29) < 0.35
     assert abs(tau.mean() - 3.63) < 0.4 and abs(tau.std() - 3.21) < 0.6
     assert abs(tb0.mean() - 0.32) < 0.1 and abs(tb0.std() - 0.99) < 0.1
+
+
+@pytest.mark.parametrize("N,K,seed", [(500, 25, 26), (5000, 25, 26), (77, 10, 5)])
+def test_diamonds_suffstat_potential(N, K, seed, orc):
+    """The sufficient-statistics potential against the literal float64 model
+    and against the direct float32 contraction, near the posterior mode and
+    far from it.  Tolerance: |dU| <= 2e-6 |U| + 1e-3 (the direct float32 sum of
+    N squared residuals carries ~N * 2^-24 relative error; the float64 form is
+    the more accurate of the two)."""
+    import posteriors as P
+    mk = P.synthetic_diamonds(N=N, K=K, seed=seed)
+    arr, _ = P.diamonds.pack_fn(mk)
+    ss, _ = P.diamonds_suffstat.pack_fn(mk)
+    om_d = orc.Model(orc.DIAMONDS, K + 1, arr, n_data=N, k_data=K)
+    om_s = orc.Model(orc.DIAMONDS_SS, K + 1, ss, n_data=N, k_data=K)
+    rng = np.random.default_rng(0)
+    Kc = K - 1
+    X = np.asarray(mk["X"], np.float64)
+    Y = np.asarray(mk["Y"], np.float64)
+    b_ls = np.linalg.lstsq(X, Y, rcond=None)[0]
+    mode = np.concatenate([[b_ls[0] + (X[:, 1:].mean(0) @ b_ls[1:])], b_ls[1:], [np.log(0.123)]])
+    z = np.concatenate([mode + 1e-3 * rng.normal(size=(200, K + 1)),
+                        rng.normal(size=(200, K + 1))]).astype(np.float32)
+    u_s = orc.potential(om_s, z).astype(np.float64)
+    u_d = orc.potential(om_d, z).astype(np.float64)
+    Xc = arr[:N * Kc].reshape(N, Kc).astype(np.float64)
+    u_l = np.array([lit.diamonds_potential(zz.astype(np.float64), Xc, arr[N * Kc:].astype(np.float64)) for zz in z])
+    tol = 2e-6 * np.abs(u_l) + 1e-3
+    assert np.all(np.abs(u_s - u_l) <= tol), np.max(np.abs(u_s - u_l) / tol)
+    assert np.all(np.abs(u_d - u_l) <= 10 * tol), np.max(np.abs(u_d - u_l) / tol)

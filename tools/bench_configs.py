@@ -56,7 +56,7 @@ def run_regime_a(name, kernel, C, d, kwargs, steps, warmup, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="diamonds,gauss256,gauss256_pooled,pooled64,asss64,asss_es,pnx")
+    ap.add_argument("--only", default="diamonds,diamonds_ss,gauss256,gauss256_pooled,pooled64,asss64,asss_es,pnx")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     args = ap.parse_args()
@@ -72,6 +72,12 @@ def main():
         k = ARWMH(model=P.diamonds, num_chains=C, device=dev)
         print(json.dumps(run_regime_a("diamonds (BASELINE configs[2])", k, C, P.diamonds.dim(data), data,
                                       args.steps, args.warmup, dev)), flush=True)
+    if "diamonds_ss" in want:
+        data = P.synthetic_diamonds()
+        C = 262144
+        k = ARWMH(model=P.diamonds_suffstat, num_chains=C, device=dev)
+        print(json.dumps(run_regime_a("diamonds, sufficient-statistics likelihood (BASELINE configs[2])", k, C,
+                                      P.diamonds_suffstat.dim(data), data, args.steps, args.warmup, dev)), flush=True)
     if "gauss256" in want:
         g = P.correlated_gaussian(256, log10_kappa=4.0)
         C = 32768
