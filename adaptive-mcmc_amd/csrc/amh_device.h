@@ -535,7 +535,7 @@ struct DiamondsSSM {
     const double quad = bi * __builtin_fma(2.0, rr, gii * bi);
     const double lin = bi * __builtin_fma(-a, sxi, ti);
     double v = act ? __builtin_fma(-2.0, lin, quad) : 0.0;
-    static_for<5>([&](auto S) {  // xor butterfly over the group (oracle dgroup_sum)
+    static_for<6>([&](auto S) {  // xor butterfly over the group (oracle dgroup_sum)
       constexpr int off = 1 << S;
       if constexpr (off < G) v = v + __shfl_xor(v, off, G);
     });

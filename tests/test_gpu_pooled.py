@@ -45,6 +45,7 @@ def _run(kind, d, C, steps, gpu, orc, seed=0, K=1):
 @pytest.mark.parametrize("kind,d,C,steps", [("gaussian", 64, 3000, 6), ("gaussian", 64, 70000, 3),
                                             ("gaussian", 7, 517, 8), ("eight_schools", None, 64, 8),
                                             ("kidiq", None, 100, 5), ("diamonds", None, 40, 3),
+                                            ("diamonds_ss", None, 1000, 4),
                                             ("gaussian", 128, 700, 4), ("gaussian", 256, 600, 3)])
 def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
     _run(kind, d, C, steps, gpu, orc)
@@ -73,7 +74,8 @@ def test_pooled_inplace_multistep(d, C, gpu, orc):
 
 @pytest.mark.parametrize("kind,d,C,blocks,K", [("gaussian", 64, 3000, 3, 4), ("gaussian", 64, 70000, 2, 16),
                                                ("gaussian", 7, 517, 3, 5), ("eight_schools", None, 64, 3, 16),
-                                               ("diamonds", None, 40, 2, 3), ("gaussian", 128, 700, 2, 3),
+                                               ("diamonds", None, 40, 2, 3), ("diamonds_ss", None, 1000, 2, 4),
+                                               ("gaussian", 128, 700, 2, 3),
                                                ("gaussian", 256, 600, 2, 2)])
 def test_pooled_blocks_bitexact(kind, d, C, blocks, K, gpu, orc):
     """sync_every = K (one update per K transitions): per-chain state, the
