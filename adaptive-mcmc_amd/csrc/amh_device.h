@@ -487,13 +487,37 @@ struct DiamondsSSM {
     }
   }
   static __device__ __forceinline__ Ctx prepare(const ModelArgs&, int, int) { return Ctx{}; }
+  // float64 Grp::sum: the same DPP / swizzle partners on both halves
+  template <int CTRL>
+  static __device__ __forceinline__ double dpp_d(double v) {
+    const f32x2v h = __builtin_bit_cast(f32x2v, v);
+    return __builtin_bit_cast(double, f32x2v{dppf<CTRL>(0.0f, h[0]), dppf<CTRL>(0.0f, h[1])});
+  }
+  template <int PATTERN>
+  static __device__ __forceinline__ double swz_d(double v) {
+    const f32x2v h = __builtin_bit_cast(f32x2v, v);
+    return __builtin_bit_cast(double, f32x2v{swz<PATTERN>(h[0]), swz<PATTERN>(h[1])});
+  }
+  static __device__ __forceinline__ double dsum(double v) {
+    if constexpr (G >= 2) v = v + dpp_d<dpp::quad(1, 0, 3, 2)>(v);
+    if constexpr (G >= 4) v = v + dpp_d<dpp::quad(2, 3, 0, 1)>(v);
+    if constexpr (G >= 8) v = v + swz_d<0x1F | (4 << 10)>(v);
+    if constexpr (G >= 16) v = v + dpp_d<dpp::kRowRor0 + 8>(v);
+    if constexpr (G >= 32) v = v + swz_d<0x1F | (16 << 10)>(v);
+    if constexpr (G == 64) v = v + __shfl_xor(v, 32, 64);
+    return v;
+  }
   static __device__ __forceinline__ double lo(const f32x4& q) { return __builtin_bit_cast(double, f32x2v{q[0], q[1]}); }
   static __device__ __forceinline__ double hi(const f32x4& q) { return __builtin_bit_cast(double, f32x2v{q[2], q[3]}); }
   static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx&, const float* lds) {
     const int Kc = d - 2;
     const int L = ldr(Kc);
     const float icpt = Grp<G>::template bcast<0>(x);
-    const float ls = Grp<G>::bcast_rt(x, Kc + 1);
+    // lane Kc + 1 (log sigma): a compile-time DPP broadcast once d is fixed
+    float ls = 0.0f;
+    static_for<G>([&](auto J) {
+      if (J == Kc + 1) ls = Grp<G>::template bcast<J>(x);
+    });
     const float sg = amh_expf(ls);
     const float isg = 1.0f / sg;
     const bool act = r >= 1 && r <= Kc;
@@ -535,10 +559,7 @@ struct DiamondsSSM {
     const double quad = bi * __builtin_fma(2.0, rr, gii * bi);
     const double lin = bi * __builtin_fma(-a, sxi, ti);
     double v = act ? __builtin_fma(-2.0, lin, quad) : 0.0;
-    static_for<6>([&](auto S) {  // xor butterfly over the group (oracle dgroup_sum)
-      constexpr int off = 1 << S;
-      if constexpr (off < G) v = v + __shfl_xor(v, off, G);
-    });
+    v = dsum(v);  // xor butterfly over the group (oracle dgroup_sum)
     const double qa = __builtin_fma(a, __builtin_fma(N, a, -2.0 * sT), A);
     const double q = qa + v;
     const double isgd = (double)isg;
