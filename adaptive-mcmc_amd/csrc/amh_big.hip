@@ -228,6 +228,12 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
 }
 
 // ---------------------------------------------------------------- step ----
+// NEXT: the pass that streams L' out also runs the next transition's propose
+// pass on the columns of L' as they are formed (the same float ops as
+// big_propose_kernel on the stored values), so a multi-step launch reads the
+// factor once per transition.  The wave's own xprop / wa / wr rows were read
+// at the top of its chain, so the next ones overwrite them in place.
+template <bool NEXT>
 __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -301,6 +307,48 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     const bool revert = __ballot(bad) != 0ull;
     float sacc[kNS];
     static_for<kNS>([&](auto K) { sacc[K] = 0.0f; });
+    // next transition's propose state (big_propose_kernel on the output state)
+    float ninv[kNS], nxi[kNS], neta[kNS], nacc[kNS], nsa[kNS], nsr[kNS], nzp[kNS], nwa[kNS], nwr[kNS];
+    if constexpr (NEXT) {
+      static_for<kNS>([&](auto K) {
+        const int r = 64 * K + lane;
+        const bool act = r < d;
+        const float ndl = act ? (revert ? dl[K] : 1.0f * qq[K]) : 0.0f;
+        ninv[K] = (amh_isfinite(ndl) && ndl != 0.0f) ? 1.0f / ndl : 0.0f;
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)itr, 0u, AMH_TAG_STEP, k0, k1);
+        nxi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+        neta[K] = ndl * nxi[K];
+        nacc[K] = nsa[K] = nsr[K] = nzp[K] = nwa[K] = nwr[K] = 0.0f;
+      });
+    }
+    // column j of L' (rows > j in nv) into the next proposal and both solves
+    auto next_col = [&](auto KB, int j, const float (&nv)[kNS]) {
+      if constexpr (NEXT) {
+        constexpr int kb = KB;
+        const int jl = j - 64 * kb;
+        const float etaj = rdl(neta[kb], jl);
+        const float invj = rdl(ninv[kb], jl);
+        if (lane == jl) {
+          nacc[kb] = fmaf(1.0f, etaj, nacc[kb]);
+          nzp[kb] = zn[kb] + fmaf(e1, nacc[kb], p.eps * nxi[kb]);
+          nwa[kb] = (nzp[kb] - mun[kb]) - nsa[kb];
+          nwr[kb] = (zn[kb] - mun[kb]) - nsr[kb];
+        }
+        const float waj = rdl(nwa[kb], jl);
+        const float wrj = rdl(nwr[kb], jl);
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r > j && r < d) {
+              const float uo = nv[K] * invj;
+              nacc[K] = fmaf(uo, etaj, nacc[K]);
+              nsa[K] = fmaf(uo, waj, nsa[K]);
+              nsr[K] = fmaf(uo, wrj, nsr[K]);
+            }
+          }
+        });
+      }
+    };
     if (!revert) {
       float ac[kNS], bc[kNS], sv[kNS];
       static_for<kNS>([&](auto K) {
@@ -319,7 +367,9 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
           sacc[kb] = fmaf(tt, tt, sacc[kb]);
           ocol[j] = 1.0f * qj;
         }
+        float nv[kNS];
         static_for<kNS>([&](auto K) {
+          nv[K] = 0.0f;
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r > j && r < d) {
@@ -329,10 +379,12 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
               const float un = fmaf(cj, w, uo);
               const float tt = fmaf(uo, acj, bcj * w);
               sacc[K] = fmaf(tt, tt, sacc[K]);
-              ocol[r] = un * qj;
+              nv[K] = un * qj;
+              ocol[r] = nv[K];
             }
           }
         });
+        next_col(KB, j, nv);
       });
     } else {
       // factor kept (arwmh.py:191): copied verbatim; as_change = ||L (e1 - e0)||_F
@@ -359,6 +411,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
             }
           }
         });
+        next_col(KB, j, v);
       });
     }
     const float asc = sqrtf(big_sum(sacc));
@@ -368,6 +421,11 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
         p.out.z[c * d + r] = zn[K];
         p.out.loc[c * d + r] = mun[K];
         if (p.col_z != nullptr) p.col_z[c * d + r] = zn[K];
+        if constexpr (NEXT) {
+          p.xprop[c * d + r] = nzp[K];
+          p.wa[c * d + r] = nwa[K];
+          p.wr[c * d + r] = nwr[K];
+        }
       }
     });
     if (lane == 0) {
@@ -496,8 +554,12 @@ hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
   hipLaunchKernelGGL(big_propose_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
-hipError_t run_big_step(const BigParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_step_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
+  if (next) {
+    hipLaunchKernelGGL(big_step_kernel<true>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  } else {
+    hipLaunchKernelGGL(big_step_kernel<false>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  }
   return hipGetLastError();
 }
 hipError_t run_big_potential(const PotParams& p, hipStream_t s) {

@@ -24,6 +24,7 @@ struct amh_handle {
   double* partials = nullptr;  // pooled mode: chunk partial sums (scratch)
   size_t partials_bytes = 0;
   float* split_buf = nullptr;  // split path: proposals [C][d] then U(z') [C] (scratch)
+  int64_t big_ready_C = -1;    // d > 64: split_buf holds the next proposal of the last output state (C chains)
   size_t split_bytes = 0;
   float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
   size_t upd_bytes = 0;
@@ -205,6 +206,11 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
 
 int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out, int32_t n_steps,
              const amh_collect* collect, void* stream) {
+  return amh_step_chained(h, num_chains, in, out, n_steps, collect, 0, stream);
+}
+
+int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+                     int32_t n_steps, const amh_collect* collect, int32_t flags, void* stream) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_step: null handle");
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_step: no model bound");
   if (!state_ok(in) || !state_ok(out) || num_chains < 1 || n_steps < 0)
@@ -252,20 +258,29 @@ int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_s
     float* pep = q.wr + (size_t)C * p.d;
     q.pep = pep;
     q.accept_count = p.accept_count;
+    // the caller vouches (AMH_STEP_PROPOSAL_READY) that `in` is the unchanged
+    // output of the previous call, which kept its next proposal in the scratch
+    const bool ready = (flags & AMH_STEP_PROPOSAL_READY) && h->big_ready_C == C;
+    const bool keep_next = (flags & AMH_STEP_KEEP_PROPOSAL) != 0;
+    h->big_ready_C = -1;
     for (int32_t t = 0; t < n_steps; ++t) {
       q.in = (t == 0) ? *in : *out;
       const bool keep = ((t + 1) % p.thinning) == 0;
       const int64_t k = t / p.thinning;
       q.col_z = (keep && p.col_z) ? p.col_z + (size_t)k * C * p.d : nullptr;
       q.col_pe = (keep && p.col_pe) ? p.col_pe + (size_t)k * C : nullptr;
-      e = amh::run_big_propose(q, (hipStream_t)stream);
+      // the first transition's proposal comes from the propose pass (or the
+      // previous call); each step pass forms the next one on the fly, so the
+      // factor is read once per transition
+      if (t == 0 && !ready) e = amh::run_big_propose(q, (hipStream_t)stream);
       if (e == hipSuccess) {
         amh::PotParams pp{q.xprop, pep, C, p.d, h->model};
         e = amh::run_big_potential(pp, (hipStream_t)stream);
       }
-      if (e == hipSuccess) e = amh::run_big_step(q, (hipStream_t)stream);
+      if (e == hipSuccess) e = amh::run_big_step(q, (hipStream_t)stream, t + 1 < n_steps || keep_next);
       if (e != hipSuccess) return hip_fail(h, e, "amh_step(d > 64)");
     }
+    h->big_ready_C = keep_next ? C : -1;
     return AMH_OK;
   }
   if (amh::split_model(h->model_id, p.d)) {
@@ -275,6 +290,7 @@ int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_s
     const size_t need = (size_t)C * (size_t)(p.d + 1) * sizeof(float);
     int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_step/hipMalloc");
     if (rc != AMH_OK) return rc;
+    h->big_ready_C = -1;
     float* xprop = h->split_buf;
     float* peprop = h->split_buf + (size_t)C * p.d;
     amh::StepParams q = p;
@@ -499,6 +515,7 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
   p.k_steps = k_steps;
   if (big) {
     const size_t nb = (size_t)num_chains * (size_t)(d + 1) * sizeof(float);
+    h->big_ready_C = -1;
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;
     // one launch sequence per step of the block, the sums accumulated

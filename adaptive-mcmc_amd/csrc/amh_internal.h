@@ -153,7 +153,8 @@ struct BigParams {
 bool big_model(int model_id, int d);
 hipError_t run_big_init(const InitParams& p, hipStream_t s);
 hipError_t run_big_propose(const BigParams& p, hipStream_t s);
-hipError_t run_big_step(const BigParams& p, hipStream_t s);
+// next: also form the next transition's proposal and solves (multi-step launches)
+hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next = false);
 hipError_t run_big_potential(const PotParams& p, hipStream_t s);
 
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain

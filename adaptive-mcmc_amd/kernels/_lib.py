@@ -21,10 +21,12 @@ AMH_MODEL_EIGHT_SCHOOLS = 2
 AMH_MODEL_KIDIQ = 3
 AMH_MODEL_DIAMONDS = 4
 AMH_MODEL_DIAMONDS_SS = 5
+AMH_STEP_PROPOSAL_READY = 1
+AMH_STEP_KEEP_PROPOSAL = 2
 
 # every symbol include/amh.h declares
 EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bind_model", "amh_init",
-           "amh_step", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
+           "amh_step", "amh_step_chained", "amh_potential", "amh_sample_pnx", "amh_chain_keys", "amh_pooled_sums_size",
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
@@ -77,6 +79,9 @@ def lib():
     L.amh_init.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), I64, I64, P, ctypes.POINTER(AmhState), P]
     L.amh_step.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), I32,
                            ctypes.POINTER(AmhCollect), P]
+    L.amh_step_chained.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), I32,
+                                   ctypes.POINTER(AmhCollect), I32, P]
+    L.amh_step_chained.restype = ctypes.c_int
     L.amh_potential.argtypes = [P, P, P, I64, P]
     L.amh_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, F, I32, P, P]
     L.amh_chain_keys.argtypes = [ctypes.POINTER(ctypes.c_uint32), I64, I64, P, P]

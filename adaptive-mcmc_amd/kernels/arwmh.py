@@ -254,16 +254,38 @@ class ARWMH:
         self._launch(state, out, n_steps, (cz, cp, thinning))
         return out, cz, cp
 
+    @staticmethod
+    def _leaves(state):
+        a = state.adapt_state
+        return (state.i, state.z, state.potential_energy, state.mean_accept_prob, a.loc, a.scale,
+                a.log_step_size, state.as_change, state.rng_key)
+
     def _launch(self, sin, sout, n_steps, collect):
         cz, cp, thin = collect if collect is not None else (None, None, 1)
         col = _lib.AmhCollect(cz.data_ptr() if cz is not None else None,
                               cp.data_ptr() if cp is not None else None,
                               self.accept_count.data_ptr() if self.accept_count is not None else None, thin)
         dev = sin.z.device.index
+        flags = 0
+        if self._dim > 64:
+            # d > 64: the step pass forms the next proposal (amh_step_chained).
+            # It is reused only for the very tensors the last call returned,
+            # unmodified since (torch's in-place version counters), which this
+            # object keeps alive so their storage cannot be recycled.
+            leaves = self._leaves(sin)
+            last = getattr(self, "_chained", None)
+            if last is not None and all(a is b for a, b in zip(leaves, last[0])) and \
+                    all(t._version == v for t, v in zip(leaves, last[1])):
+                flags |= _lib.AMH_STEP_PROPOSAL_READY
+            flags |= _lib.AMH_STEP_KEEP_PROPOSAL
+            self._chained = None
         with torch.cuda.device(dev):
-            _lib.check(_lib.lib().amh_step(self._handle.h, sin.z.shape[0], ctypes_state(self, sin),
-                                           ctypes_state(self, sout), n_steps, col, _lib.stream_ptr(dev)),
-                       self._handle.h)
+            _lib.check(_lib.lib().amh_step_chained(self._handle.h, sin.z.shape[0], ctypes_state(self, sin),
+                                                   ctypes_state(self, sout), n_steps, col, flags,
+                                                   _lib.stream_ptr(dev)), self._handle.h)
+        if flags:
+            out = self._leaves(sout)
+            self._chained = (out, tuple(t._version for t in out))
 
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""

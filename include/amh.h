@@ -118,6 +118,17 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
 int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
              int32_t n_steps, const amh_collect* collect, void* stream);
 
+/* amh_step with flags (64 < d <= 256; other shapes ignore them).  The step
+ * pass of the large-d path forms the next transition's proposal while it
+ * streams L' out; AMH_STEP_KEEP_PROPOSAL keeps the one after the last step in
+ * the handle, and AMH_STEP_PROPOSAL_READY tells the next call that its `in` is
+ * that unchanged output (same chains), so its propose pass is skipped.  The
+ * handle drops a kept proposal whenever its scratch is used otherwise, and
+ * READY without one falls back to the propose pass.  Same bits either way. */
+enum { AMH_STEP_PROPOSAL_READY = 1, AMH_STEP_KEEP_PROPOSAL = 2 };
+int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+                     int32_t n_steps, const amh_collect* collect, int32_t flags, void* stream);
+
 /* potential_fn(z) for n points: pe[n] from z[n][d] (arwmh.py:121). */
 int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* stream);
 

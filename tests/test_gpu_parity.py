@@ -267,3 +267,29 @@ def test_diamonds_suffstat_generic_k(gpu, orc):
     z = np.random.default_rng(2).normal(size=(300, K + 1)).astype(np.float32)
     pe = k.potential(torch.as_tensor(z, device=gpu)).cpu().numpy()
     np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
+
+
+def test_big_dim_chained_proposal_invalidation(gpu, orc):
+    """d > 64 sample() reuses the proposal the previous step pass formed only
+    for the unchanged state it returned: an in-place edit of z between calls
+    (torch version counter) or a different state object forces the propose
+    pass, and every path stays bit-identical to the oracle."""
+    d, C = 128, 65
+    k, st, om, ost = _init("gaussian", C, gpu, orc, d=d, num_warmup=2)
+    for t in range(3):
+        st = k.sample(st, (), {})
+        orc.step(om, ost, 1, num_warmup=2)
+    st.z[:, 0] += 0.25  # in place: the kept proposal is stale
+    ost.z[:, 0] += np.float32(0.25)
+    for t in range(3):
+        st = k.sample(st, (), {})
+        orc.step(om, ost, 1, num_warmup=2)
+        torch.cuda.synchronize()
+        assert_state_bitequal(st, ost, f"after edit, step {t}")
+    other = st._replace(z=st.z.clone())  # same values, another tensor
+    st = k.sample(other, (), {})
+    orc.step(om, ost, 1, num_warmup=2)
+    k.sample_(st, 2)
+    orc.step(om, ost, 2, num_warmup=2)
+    torch.cuda.synchronize()
+    assert_state_bitequal(st, ost, "clone + in-place")
