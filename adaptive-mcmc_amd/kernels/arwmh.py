@@ -19,6 +19,7 @@ Differences a caller can see (DESIGN.md lists them with their reasons):
 """
 from __future__ import annotations
 
+import weakref
 from collections import namedtuple
 
 import numpy as np
@@ -269,12 +270,12 @@ class ARWMH:
         flags = 0
         if self._dim > 64:
             # d > 64: the step pass forms the next proposal (amh_step_chained).
-            # It is reused only for the very tensors the last call returned,
-            # unmodified since (torch's in-place version counters), which this
-            # object keeps alive so their storage cannot be recycled.
+            # It is reused only for the very tensors the last call returned
+            # (weak references: a dead one never matches, so recycled storage
+            # cannot pass), unmodified since (torch's in-place version counters).
             leaves = self._leaves(sin)
             last = getattr(self, "_chained", None)
-            if last is not None and all(a is b for a, b in zip(leaves, last[0])) and \
+            if last is not None and all(w() is t for w, t in zip(last[0], leaves)) and \
                     all(t._version == v for t, v in zip(leaves, last[1])):
                 flags |= _lib.AMH_STEP_PROPOSAL_READY
             flags |= _lib.AMH_STEP_KEEP_PROPOSAL
@@ -285,7 +286,7 @@ class ARWMH:
                                                    _lib.stream_ptr(dev)), self._handle.h)
         if flags:
             out = self._leaves(sout)
-            self._chained = (out, tuple(t._version for t in out))
+            self._chained = (tuple(weakref.ref(t) for t in out), tuple(t._version for t in out))
 
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""
