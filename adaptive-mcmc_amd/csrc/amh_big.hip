@@ -178,10 +178,12 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
     const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
     const float el = amh_expf(p.in.log_step_size[c]);
     float inv[kNS], xi[kNS], eta[kNS], zz[kNS], mu[kNS], acc[kNS], sa[kNS], sr[kNS], zp[kNS], wa[kNS], wr[kNS];
+    float pdl[kNS];
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       const float dl = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
+      pdl[K] = dl;
       inv[K] = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
       const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
       xi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
@@ -222,6 +224,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
         p.xprop[c * d + r] = zp[K];
         p.wa[c * d + r] = wa[K];
         p.wr[c * d + r] = wr[K];
+        p.dg[c * d + r] = pdl[K];
       }
     });
   }
@@ -269,7 +272,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
-      dl[K] = act ? Lin[col_off(d, act ? r : 0)] : 0.0f;
+      dl[K] = act ? p.dg[c * d + r] : 0.0f;  // the diagonal, coalesced (propose / previous step pass)
       inv[K] = (amh_isfinite(dl[K]) && dl[K] != 0.0f) ? 1.0f / dl[K] : 0.0f;
       const float z = act ? p.in.z[c * d + r] : 0.0f;
       const float mu = act ? p.in.loc[c * d + r] : 0.0f;
@@ -308,12 +311,13 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     float sacc[kNS];
     static_for<kNS>([&](auto K) { sacc[K] = 0.0f; });
     // next transition's propose state (big_propose_kernel on the output state)
-    float ninv[kNS], nxi[kNS], neta[kNS], nacc[kNS], nsa[kNS], nsr[kNS], nzp[kNS], nwa[kNS], nwr[kNS];
+    float ninv[kNS], nxi[kNS], neta[kNS], nacc[kNS], nsa[kNS], nsr[kNS], nzp[kNS], nwa[kNS], nwr[kNS], ndg[kNS];
     if constexpr (NEXT) {
       static_for<kNS>([&](auto K) {
         const int r = 64 * K + lane;
         const bool act = r < d;
         const float ndl = act ? (revert ? dl[K] : 1.0f * qq[K]) : 0.0f;
+        ndg[K] = ndl;
         ninv[K] = (amh_isfinite(ndl) && ndl != 0.0f) ? 1.0f / ndl : 0.0f;
         const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)itr, 0u, AMH_TAG_STEP, k0, k1);
         nxi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
@@ -425,6 +429,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
           p.xprop[c * d + r] = nzp[K];
           p.wa[c * d + r] = nwa[K];
           p.wr[c * d + r] = nwr[K];
+          p.dg[c * d + r] = ndg[K];
         }
       }
     });

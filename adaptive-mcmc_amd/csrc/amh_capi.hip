@@ -239,7 +239,7 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
   if (amh::big_model(h->model_id, p.d)) {
     // d > 64: propose pass, MFMA potential, step pass per transition
     const int64_t C = num_chains;
-    const size_t need = (size_t)C * (size_t)(3 * p.d + 1) * sizeof(float);
+    const size_t need = (size_t)C * (size_t)(4 * p.d + 1) * sizeof(float);
     int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_step/hipMalloc");
     if (rc != AMH_OK) return rc;
     amh::BigParams q{};
@@ -255,7 +255,8 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
     q.xprop = h->split_buf;
     q.wa = q.xprop + (size_t)C * p.d;
     q.wr = q.wa + (size_t)C * p.d;
-    float* pep = q.wr + (size_t)C * p.d;
+    q.dg = q.wr + (size_t)C * p.d;
+    float* pep = q.dg + (size_t)C * p.d;
     q.pep = pep;
     q.accept_count = p.accept_count;
     // the caller vouches (AMH_STEP_PROPOSAL_READY) that `in` is the unchanged

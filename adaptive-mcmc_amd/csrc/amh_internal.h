@@ -145,6 +145,7 @@ struct BigParams {
   const float* gamma_tab;
   int32_t gamma_tab_n;
   float *xprop, *wa, *wr;  // propose -> step scratch [C][d]
+  float* dg;               // the factor's diagonal [C][d] (propose / step<NEXT> -> step)
   const float* pep;        // U(z') [C]
   int32_t* accept_count;   // [C] or null
   float* col_z;            // this step's collection slot [C][d] or null
