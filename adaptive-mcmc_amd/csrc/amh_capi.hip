@@ -25,6 +25,7 @@ struct amh_handle {
   size_t partials_bytes = 0;
   float* split_buf = nullptr;  // split path: proposals [C][d] then U(z') [C] (scratch)
   int64_t big_ready_C = -1;    // d > 64: split_buf holds the next proposal of the last output state (C chains)
+  amh_state big_ready_out{};   // ... and that output state's buffers: READY is honoured only for these
   size_t split_bytes = 0;
   float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
   size_t upd_bytes = 0;
@@ -42,6 +43,12 @@ int fail(amh_handle* h, int code, const std::string& msg) {
 
 int hip_fail(amh_handle* h, hipError_t e, const char* where) {
   return fail(h, AMH_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+bool same_buffers(const amh_state& a, const amh_state& b) {
+  return a.i == b.i && a.z == b.z && a.potential_energy == b.potential_energy &&
+         a.mean_accept_prob == b.mean_accept_prob && a.loc == b.loc && a.scale == b.scale &&
+         a.log_step_size == b.log_step_size && a.as_change == b.as_change && a.rng_key == b.rng_key;
 }
 
 bool state_ok(const amh_state* s) {
@@ -215,7 +222,10 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_step: no model bound");
   if (!state_ok(in) || !state_ok(out) || num_chains < 1 || n_steps < 0)
     return fail(h, AMH_EINVAL, "amh_step: bad arguments");
-  if (n_steps == 0) return AMH_OK;
+  if (n_steps == 0) {
+    h->big_ready_C = -1;  // a kept proposal never survives a call it was not used in
+    return AMH_OK;
+  }
   if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_step: thinning must be >= 1");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_step/hipSetDevice");
@@ -261,7 +271,8 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
     q.accept_count = p.accept_count;
     // the caller vouches (AMH_STEP_PROPOSAL_READY) that `in` is the unchanged
     // output of the previous call, which kept its next proposal in the scratch
-    const bool ready = (flags & AMH_STEP_PROPOSAL_READY) && h->big_ready_C == C;
+    // (and `in` must be the very buffers that call wrote)
+    const bool ready = (flags & AMH_STEP_PROPOSAL_READY) && h->big_ready_C == C && same_buffers(*in, h->big_ready_out);
     const bool keep_next = (flags & AMH_STEP_KEEP_PROPOSAL) != 0;
     h->big_ready_C = -1;
     for (int32_t t = 0; t < n_steps; ++t) {
@@ -282,6 +293,7 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
       if (e != hipSuccess) return hip_fail(h, e, "amh_step(d > 64)");
     }
     h->big_ready_C = keep_next ? C : -1;
+    h->big_ready_out = *out;
     return AMH_OK;
   }
   if (amh::split_model(h->model_id, p.d)) {

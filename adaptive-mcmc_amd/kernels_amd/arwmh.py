@@ -129,6 +129,7 @@ class ARWMH:
         self._model_kwargs = None
         self._dim = None
         self.accept_count = None  # [C] int32 accepted proposals since init (diagnostic)
+        self.chain_proposals = True  # d > 64: reuse the step pass's next proposal across sample() calls
 
     @property
     def model(self):
@@ -247,6 +248,8 @@ class ARWMH:
         """Fused n_steps transitions (numpyro fori_collect over sample); returns
         (new_state, z [n_steps // thinning, C, d] or None, pe or None)."""
         C = self._check_state(state)
+        if int(n_steps) == 0:  # nothing to run: a copy of the input, no collections
+            return _clone_state(state), None, None
         out = self._alloc_state(C, self._dim, state.z.device)
         keep = n_steps // thinning
         dev = state.z.device
@@ -262,17 +265,23 @@ class ARWMH:
                 a.log_step_size, state.as_change, state.rng_key)
 
     def _launch(self, sin, sout, n_steps, collect):
+        if int(n_steps) == 0:
+            return  # no launch: the chained proposal (if any) stays with the tensors it was made for
         cz, cp, thin = collect if collect is not None else (None, None, 1)
         col = _lib.AmhCollect(cz.data_ptr() if cz is not None else None,
                               cp.data_ptr() if cp is not None else None,
                               self.accept_count.data_ptr() if self.accept_count is not None else None, thin)
         dev = sin.z.device.index
         flags = 0
-        if self._dim > 64:
+        if self._dim > 64 and self.chain_proposals and not any(t.is_inference() for t in self._leaves(sin)):
             # d > 64: the step pass forms the next proposal (amh_step_chained).
             # It is reused only for the very tensors the last call returned
             # (weak references: a dead one never matches, so recycled storage
-            # cannot pass), unmodified since (torch's in-place version counters).
+            # cannot pass), unmodified since (torch's in-place version counters;
+            # inference-mode tensors have none, so they are never chained).
+            # Edits that bypass the version counter (`.data`, DLPack) are not
+            # seen: set `chain_proposals = False` when state is edited that way.
+            # The library checks too: READY holds only for the buffers it wrote.
             leaves = self._leaves(sin)
             last = getattr(self, "_chained", None)
             if last is not None and all(w() is t for w, t in zip(last[0], leaves)) and \
@@ -286,7 +295,10 @@ class ARWMH:
                                                    _lib.stream_ptr(dev)), self._handle.h)
         if flags:
             out = self._leaves(sout)
-            self._chained = (tuple(weakref.ref(t) for t in out), tuple(t._version for t in out))
+            if any(t.is_inference() for t in out):
+                self._chained = None
+            else:
+                self._chained = (tuple(weakref.ref(t) for t in out), tuple(t._version for t in out))
 
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""
@@ -343,6 +355,13 @@ class ARWMH:
         if self._model is None:
             return z
         return self._model.unravel(z, self._model_kwargs)
+
+
+def _clone_state(s: ARWMHState) -> ARWMHState:
+    a = s.adapt_state
+    return ARWMHState(s.i.clone(), s.z.clone(), s.potential_energy.clone(), s.mean_accept_prob.clone(),
+                      ARWMHAdaptState(a.loc.clone(), a.scale.clone(), a.log_step_size.clone()),
+                      s.as_change.clone(), s.rng_key.clone())
 
 
 def ctypes_state(kernel: ARWMH, s: ARWMHState):

@@ -8,7 +8,7 @@ ASSSState / ASSSAdaptState, with a leading chain axis on every leaf.  Every
 transition of every chain runs in the HIP kernel amh_asss.hip (C-ABI
 amh_asss_step / amh_asss_sample_pnx, include/amh.h); there is no CPU path.
 
-Differences a caller can see are those of ARWMH (kernels/arwmh.py): torch
+Differences a caller can see are those of ARWMH (kernels_amd/arwmh.py): torch
 leaves on the GPU, packed column-major `scale`, counter-based Philox noise
 (`rng_key` fixed per chain, stream position `i`), registry models.
 """

@@ -21,7 +21,7 @@ from typing import Callable, Dict, List, Tuple
 import numpy as np
 import torch
 
-from kernels import _lib
+from kernels_amd import _lib
 
 
 @dataclass

@@ -33,8 +33,8 @@ import math
 import numpy as np
 import torch
 
-from kernels import _lib
-from kernels.random import as_key
+from kernels_amd import _lib
+from kernels_amd.random import as_key
 
 __all__ = ["pth_moment_rmse", "wasserstein_dist11_p", "wasserstein_1d", "max_sliced_wasserstein", "gaussian_kernel",
            "mmd2_unbiased", "mmd_heuristic"]

@@ -14,7 +14,7 @@ from typing import List
 import numpy as np
 import torch
 
-from kernels.arwmh import ARWMHAdaptState, ARWMHState
+from kernels_amd.arwmh import ARWMHAdaptState, ARWMHState
 
 
 def ns_logscale(n_pow: int = 6) -> np.ndarray:

@@ -30,7 +30,7 @@ import numpy as np
 import torch
 import torch.nn as nn
 
-from kernels.random import as_key, split
+from kernels_amd.random import as_key, split
 
 __all__ = ["spectral_norm", "SpectralNormDense", "LipschitzNN", "compute_wasserstein_contraction",
            "compute_kernel_distance", "compute_kernel_distance_1d"]

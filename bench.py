@@ -36,8 +36,8 @@ def bytes_per_chain_step(d: int) -> int:
 
 def ess_of(x: np.ndarray) -> float:
     """Multi-chain ESS of x [chains, draws] (numpyro's estimator, the n_eff
-    of print_summary: adaptive-mcmc_amd/infer/diagnostics.py)."""
-    from infer.diagnostics import effective_sample_size
+    of print_summary: adaptive-mcmc_amd/infer_amd/diagnostics.py)."""
+    from infer_amd.diagnostics import effective_sample_size
     return float(effective_sample_size(x))
 
 
@@ -64,7 +64,7 @@ def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int,
     one all-reduce and refactorisation per K transitions."""
     import torch
     import torch.distributed as dist
-    from kernels import PooledARWMH, PRNGKey
+    from kernels_amd import PooledARWMH, PRNGKey
     K = sync_every
     steps, warmup = -(-steps // K) * K, -(-warmup // K) * K
     k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=rank * C, sync_every=K)
@@ -98,7 +98,7 @@ def cpu_baseline(g, d: int, budget_s: float = 12.0):
     steps as fit the time budget (at least one)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import orc
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     data, _ = g.pack("cpu")
     om = orc.Model(orc.GAUSSIAN, d, data.numpy())
     C = 65536
@@ -144,9 +144,9 @@ def main():
     dev = torch.device("cuda", local)
 
     import posteriors as P
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
 
-    from kernels.distributed import shard_range
+    from kernels_amd.distributed import shard_range
     d, C = args.dim, args.chains
     off = rank * C
     strong = args.total_chains > 0

@@ -19,7 +19,7 @@ def header_symbols():
 
 @pytest.fixture(scope="module")
 def lib():
-    from kernels import _lib
+    from kernels_amd import _lib
     if not os.path.exists(_lib.LIB_PATH):
         _lib.build()
     return _lib

@@ -8,7 +8,7 @@ import pytest
 import torch
 
 import posteriors as P
-from kernels import ARWMH, PRNGKey, pack_scale, packed_size, split, unpack_scale
+from kernels_amd import ARWMH, PRNGKey, pack_scale, packed_size, split, unpack_scale
 
 
 def test_model_xor_potential_fn():

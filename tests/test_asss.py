@@ -17,7 +17,7 @@ from test_oracle import lit_potential, unpack
 
 def _step_compare(kind, pre, orc, C=48, d=None):
     _, _, om = make_case(kind, d)
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     st = orc.init(om, PRNGKey(7), C)
     if pre:
         orc.asss_step(om, st, pre)
@@ -59,7 +59,7 @@ def test_oracle_step_matches_literal(kind, d, pre, orc):
 def test_first_step_keeps_factor(orc):
     """gamma_1 = 1: sqrt(1-gamma) L = 0 -> NaN -> keep L; mu jumps to x'."""
     _, _, om = make_case("eight_schools")
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     st = orc.init(om, PRNGKey(1), 16)
     L0 = st.scale.copy()
     orc.asss_step(om, st, 1)
@@ -84,7 +84,7 @@ def test_gaussian_moments(orc):
                                               [0, 0, 0.1, 1.0]]))
     data, _ = g.pack("cpu")
     om = O.Model(O.GAUSSIAN, 4, data.numpy())
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     st = orc.init(om, PRNGKey(2), 256)
     orc.asss_step(om, st, 300)
     cz, _ = orc.asss_step(om, st, 400, collect_z=True)

@@ -1,4 +1,4 @@
-"""Chain sharding (kernels/distributed.py) with world_size 2 over gloo on the
+"""Chain sharding (kernels_amd/distributed.py) with world_size 2 over gloo on the
 CPU: shard ranges tile the global chain ids, and two ranks running their
 shards with chain_offset reproduce the unsharded run bit for bit (the C
 oracle stands in for the device step here; tests/test_gpu_parity.py checks
@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch.multiprocessing as mp
 
-from kernels.distributed import shard_range
+from kernels_amd.distributed import shard_range
 
 
 def test_shard_range_tiles():
@@ -40,8 +40,8 @@ def _worker(rank, world, port, C, steps, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import orc
     from helpers import make_case
-    from kernels import PRNGKey
-    from kernels.distributed import gather_chains, max_over_ranks, shard_range
+    from kernels_amd import PRNGKey
+    from kernels_amd.distributed import gather_chains, max_over_ranks, shard_range
     _, _, om = make_case("gaussian", 8)
     off, cnt = shard_range(C, rank, world)
     st = orc.init(om, PRNGKey(7), cnt, chain_offset=off)
@@ -58,7 +58,7 @@ def _worker(rank, world, port, C, steps, out_path):
 
 def test_sharded_run_equals_unsharded(tmp_path, orc):
     from helpers import make_case
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     C, steps = 101, 25
     out = str(tmp_path / "g.npz")
     mp.start_processes(_worker, args=(2, _free_port(), C, steps, out), nprocs=2, join=True, start_method="spawn")

@@ -32,7 +32,7 @@ def assert_bitequal(st, ost, what):
 
 
 def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
-    from kernels import ASSS, PRNGKey
+    from kernels_amd import ASSS, PRNGKey
     kw, mk, om = make_case(kind, d)
     k = ASSS(num_chains=C, **kw)
     key = PRNGKey(seed)
@@ -81,7 +81,7 @@ def test_asss_fused_and_collect_bitexact(kind, d, C, gpu, orc):
 
 
 def test_asss_sample_pnx_bitexact(gpu, orc):
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     k, st, om, ost = _init("eight_schools", 64, orc)
     k.sample_(st, 300)
     a = st.adapt_state
@@ -98,8 +98,8 @@ def test_asss_eight_schools_posterior(gpu):
     mu 4.46 (sd 3.30), tau 3.54 (3.20), theta_base[0] 0.31 (0.98); on 256
     chains (2.56M kept draws) through infer.MCMC."""
     import posteriors as P
-    from infer import MCMC
-    from kernels import ASSS, PRNGKey
+    from infer_amd import MCMC
+    from kernels_amd import ASSS, PRNGKey
     k = ASSS(model=P.eight_schools, num_chains=256)
     m = MCMC(k, num_warmup=25000, num_samples=250000, thinning=25)
     m.run(PRNGKey(0), extra_fields=("potential_energy",), **P.EIGHT_SCHOOLS_DATA)

@@ -1,0 +1,62 @@
+"""The reference's collect_states_logscale driver (python/utils/kernel_utils.py:20-38)
+on the device, against the committed golden trajectory (tests/golden/eight_schools.npz,
+made by the literal float64 restatement, tests/golden/make_golden.py).
+
+4 chains of eight schools, n_pow = 3: 1,000 steps with W = 0 and the state
+recorded at the 190 grid points of ns_logscale(3), exactly the golden file's
+record.  Every thinning interval is one fused launch, so this also covers the
+fused path against the float64 literal restatement over 1,000 steps."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from test_golden import tol
+
+pytestmark = pytest.mark.gpu
+
+G = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def test_collect_states_logscale_eight_schools_golden(gpu):
+    import posteriors as P
+    from kernels_amd import ARWMH
+    from utils_amd.kernel_utils import collect_states_logscale, ns_logscale
+    f = np.load(os.path.join(G, "eight_schools.npz"))
+    d = 10
+    assert np.array_equal(ns_logscale(3), f["steps_recorded"])
+    k = ARWMH(model=P.eight_schools, num_chains=4, device=gpu)
+    st = collect_states_logscale(f["run_key"], k, dict(P.EIGHT_SCHOOLS_DATA), n_pow=3,
+                                 init_params=torch.as_tensor(f["init_z"]))
+    torch.cuda.synchronize()
+    n = len(f["steps_recorded"])
+    assert st.z.shape == (n, 4, d) and st.adapt_state.scale.shape == (n, 4, d * (d + 1) // 2)
+    assert np.array_equal(st.rng_key[0].cpu().numpy().view(np.uint32), f["chain_keys"])
+    i = st.i.cpu().numpy()
+    assert np.array_equal(i, f["i"])
+    z, loc = st.z.cpu().numpy(), st.adapt_state.loc.cpu().numpy()
+    pe = st.potential_energy.cpu().numpy()
+    lam = st.adapt_state.log_step_size.cpu().numpy()
+    macc = st.mean_accept_prob.cpu().numpy()
+    sc = st.adapt_state.scale.cpu().numpy()
+
+    def unpack(p):
+        L = np.zeros((d, d))
+        o = 0
+        for j in range(d):
+            L[j:, j] = p[o:o + d - j]
+            o += d - j
+        return L
+
+    for kk, t in enumerate(f["steps_recorded"]):
+        tl = tol(int(t))
+        np.testing.assert_allclose(z[kk], f["z"][kk], rtol=tl["z"][0], atol=tl["z"][1], err_msg=f"z t={t}")
+        np.testing.assert_allclose(loc[kk], f["loc"][kk], rtol=tl["loc"][0], atol=tl["loc"][1], err_msg=f"loc t={t}")
+        np.testing.assert_allclose(pe[kk], f["pe"][kk], rtol=tl["pe"][0], atol=tl["pe"][1], err_msg=f"pe t={t}")
+        assert np.max(np.abs(lam[kk] - f["lam"][kk])) <= tl["lam"], t
+        assert np.max(np.abs(macc[kk] - f["macc"][kk])) <= tl["macc"], t
+        for c in range(4):
+            L1, Lg = unpack(sc[kk, c]), unpack(f["scale"][kk, c])
+            S1, Sg = L1 @ L1.T, Lg @ Lg.T
+            assert np.max(np.abs(S1 - Sg)) <= 1e-3 * np.max(np.abs(Sg)) + 1e-5, (int(t), c)

@@ -25,7 +25,7 @@ def _np_mmd2_unbiased(x, y, gamma):
 
 @pytest.mark.parametrize("n,m,d", [(300, 257, 26), (129, 128, 1), (64, 500, 70)])
 def test_mmd2_unbiased_and_kernel(n, m, d, gpu):
-    from utils import evaluation as E
+    from utils_amd import evaluation as E
     rng = np.random.default_rng(n + m + d)
     x = rng.normal(size=(n, d)).astype(np.float32)
     y = (rng.normal(size=(m, d)) * 1.2 + 0.3).astype(np.float32)
@@ -40,7 +40,7 @@ def test_mmd2_unbiased_and_kernel(n, m, d, gpu):
 
 
 def test_mmd_heuristic(gpu):
-    from utils import evaluation as E
+    from utils_amd import evaluation as E
     rng = np.random.default_rng(5)
     x = rng.normal(size=(400, 10)).astype(np.float32)
     y = rng.normal(size=(301, 10)).astype(np.float32)
@@ -54,8 +54,8 @@ def test_mmd_heuristic(gpu):
 
 
 def test_sliced_and_moments(gpu):
-    from kernels import PRNGKey
-    from utils import evaluation as E
+    from kernels_amd import PRNGKey
+    from utils_amd import evaluation as E
     rng = np.random.default_rng(6)
     mu = rng.normal(size=(1000, 8)).astype(np.float32)
     nu = (rng.normal(size=(1000, 8)) + 0.5).astype(np.float32)
@@ -78,8 +78,8 @@ def test_mmd_of_asss_draws_vs_reference_sample(gpu):
     compared with a shifted sample (a use of the metrics as in the
     reference's evaluation scripts)."""
     import posteriors as P
-    from kernels import ARWMH, ASSS, PRNGKey
-    from utils import evaluation as E
+    from kernels_amd import ARWMH, ASSS, PRNGKey
+    from utils_amd import evaluation as E
     g = P.gaussian(np.zeros(4), cov=np.diag([1.0, 2.0, 0.5, 1.0]))
     draws = []
     for K in (ARWMH, ASSS):

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 def _es(gpu, C):
     import posteriors as P
-    from kernels import ARWMH
+    from kernels_amd import ARWMH
     return ARWMH(model=P.eight_schools, num_chains=C, device=gpu), dict(P.EIGHT_SCHOOLS_DATA)
 
 
@@ -19,8 +19,8 @@ def test_eight_schools_posterior(gpu):
     """The notebook's run configuration on 256 chains (2.56M kept draws, ~2 s).
     Shorter runs (5e3 warmup, 5e4 samples) sit visibly high in tau: the
     funnel's neck is reached late, in the reference's single chain as here."""
-    from infer import MCMC
-    from kernels import PRNGKey
+    from infer_amd import MCMC
+    from kernels_amd import PRNGKey
     C = 256
     k, data = _es(gpu, C)
     m = MCMC(k, num_warmup=50000, num_samples=500000, thinning=50)
@@ -44,7 +44,7 @@ def test_eight_schools_posterior(gpu):
     rows = [ln for ln in txt.split("\n") if ln.strip()]
     assert len(rows) == 1 + 1 + 1 + 8  # header, mu, tau, theta_base[0..7]; theta excluded
     assert rows[0] == "                   mean       std    median      5.0%     95.0%     n_eff     r_hat"
-    from infer import diagnostics as D
+    from infer_amd import diagnostics as D
     g = m.get_samples(group_by_chain=True)
     assert g["mu"].shape == (C, K)
     assert float(D.effective_sample_size(g["mu"])) > 0.5 * C * K
@@ -59,8 +59,8 @@ def test_thinning_and_extra_fields_paths(gpu):
     bit; the two differ only at ULP level (a fused launch keeps the factor in
     unit-lower form between its steps).  Remainder steps come
     first (numpyro fori_collect)."""
-    from infer import MCMC
-    from kernels import PRNGKey
+    from infer_amd import MCMC
+    from kernels_amd import PRNGKey
     res = []
     for fields in [("potential_energy",), ("potential_energy", "adapt_state", "mean_accept_prob")]:
         k, data = _es(gpu, 33)
@@ -98,8 +98,8 @@ def test_thinning_and_extra_fields_paths(gpu):
 
 
 def test_post_warmup_state_continues(gpu):
-    from infer import MCMC
-    from kernels import PRNGKey
+    from infer_amd import MCMC
+    from kernels_amd import PRNGKey
     k, data = _es(gpu, 16)
     m = MCMC(k, num_warmup=50, num_samples=20)
     m.warmup(PRNGKey(1), **data)
@@ -114,8 +114,8 @@ def test_post_warmup_state_continues(gpu):
 
 def test_pooled_kernel_under_mcmc(gpu):
     import posteriors as P
-    from infer import MCMC
-    from kernels import PooledARWMH, PRNGKey
+    from infer_amd import MCMC
+    from kernels_amd import PooledARWMH, PRNGKey
     g = P.correlated_gaussian(16)
     C = 256
     k = PooledARWMH(potential_fn=g, num_chains=C, device=gpu)

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _init(kind, C, gpu, orc, seed=0, d=None, num_warmup=0):
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
     kw, mk, om = make_case(kind, d)
     k = ARWMH(num_chains=C, **kw)
     key = PRNGKey(seed)
@@ -90,7 +90,7 @@ def test_split_path_generic_k(gpu, orc):
     (K = 10, ragged N = 77): collection with thinning and in-place steps
     stay bit-identical to the oracle."""
     import posteriors as P
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
     mk = P.synthetic_diamonds(N=77, K=10, seed=5)
     arr, (N, K) = P.diamonds.pack_fn(mk)
     om = orc.Model(orc.DIAMONDS, K + 1, arr, n_data=N, k_data=K)
@@ -132,7 +132,7 @@ def test_big_dim_bitexact(d, C, steps, gpu, orc):
 
 
 def test_sample_pnx_bitexact(gpu, orc):
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     k, st, om, ost = _init("gaussian", 4, gpu, orc, d=16)
     st = k.sample_(st, 50)
     ad = st.adapt_state
@@ -150,7 +150,7 @@ def test_headline_size_properties(gpu):
     """65,536 chains x d = 64 (BASELINE config 2): after 200 steps every factor
     has a positive finite diagonal, acceptance moves toward 0.234, and the
     launch is deterministic (two runs from one state agree bit for bit)."""
-    from kernels import ARWMH, PRNGKey, unpack_scale
+    from kernels_amd import ARWMH, PRNGKey, unpack_scale
     import posteriors as P
     g = P.correlated_gaussian(64)
     C = 65536
@@ -173,8 +173,8 @@ def test_headline_size_properties(gpu):
 def test_sharded_equals_unsharded(gpu):
     """Regime A sharding: two shards run with chain_offset
     reproduce the unsharded run bit for bit, including a ragged split."""
-    from kernels import ARWMH, PRNGKey
-    from kernels.distributed import shard_range
+    from kernels_amd import ARWMH, PRNGKey
+    from kernels_amd.distributed import shard_range
     import posteriors as P
     g = P.correlated_gaussian(64)
     C = 3001
@@ -198,7 +198,7 @@ def test_sharded_equals_unsharded(gpu):
 def test_edge_sizes(gpu, orc):
     """One chain, a chain count that leaves most of the last work item empty,
     and d = 1 (the frozen-acceptance model of asumptions_check.ipynb)."""
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
     import posteriors as P
     for d, C in ((64, 1), (3, 17), (1, 5), (2, 1)):
         g = P.correlated_gaussian(d)
@@ -220,7 +220,7 @@ def test_gpu_follows_golden(name, gpu):
     within the tolerances of tests/test_golden.py."""
     import os
     import posteriors as P
-    from kernels import ARWMH
+    from kernels_amd import ARWMH
     from test_golden import tol
     f = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", name + ".npz"))
     C = f["init_z"].shape[0]
@@ -251,7 +251,7 @@ def test_diamonds_suffstat_generic_k(gpu, orc):
     d = 11 in the G = 32 group): init, thinned collection and the potential
     bit-identical to the oracle."""
     import posteriors as P
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
     mk = P.synthetic_diamonds(N=77, K=10, seed=5)
     arr, (N, K) = P.diamonds_suffstat.pack_fn(mk)
     om = orc.Model(orc.DIAMONDS_SS, K + 1, arr, n_data=N, k_data=K)
@@ -293,3 +293,22 @@ def test_big_dim_chained_proposal_invalidation(gpu, orc):
     orc.step(om, ost, 2, num_warmup=2)
     torch.cuda.synchronize()
     assert_state_bitequal(st, ost, "clone + in-place")
+    # a zero-step call in between must not hand s1's kept proposal to s0
+    s0 = st
+    ost0 = ost.copy()
+    s1 = k.sample(s0, (), {})
+    k.sample_(s0, 0)
+    s0b = k.sample(s0, (), {})
+    orc.step(om, ost0, 1, num_warmup=2)
+    torch.cuda.synchronize()
+    assert_state_bitequal(s0b, ost0, "zero-step call between")
+    assert_state_bitequal(s1, ost0, "s1 = step(s0)")
+    z0 = k.run(s0b, 0)
+    assert z0[1] is None and torch.equal(z0[0].z, s0b.z) and z0[0].z.data_ptr() != s0b.z.data_ptr()
+    # inference-mode tensors carry no version counter: never chained, still exact
+    with torch.inference_mode():
+        si = k.sample(s0b, (), {})
+        si = k.sample(si, (), {})
+    orc.step(om, ost0, 2, num_warmup=2)
+    torch.cuda.synchronize()
+    assert_state_bitequal(si, ost0, "inference mode")

@@ -11,7 +11,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _run(kind, d, C, steps, gpu, orc, seed=0, K=1):
-    from kernels import PooledARWMH, PRNGKey
+    from kernels_amd import PooledARWMH, PRNGKey
     kw, mk, om = make_case(kind, d)
     k = PooledARWMH(num_chains=C, sync_every=K, **kw)
     z0 = np.random.default_rng(seed).uniform(-2, 2, size=(C, om.d)).astype(np.float32)
@@ -55,7 +55,7 @@ def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
 def test_pooled_inplace_multistep(d, C, gpu, orc):
     """sample_ (amh_pooled_step, in place: in and out states alias) equals
     repeated out-of-place sample(); covers the large-d update's staging."""
-    from kernels import PooledARWMH, PRNGKey
+    from kernels_amd import PooledARWMH, PRNGKey
     kw, mk, om = make_case("gaussian", d)
     z0 = torch.empty(C, d, device=gpu).uniform_(-2, 2)
     a = PooledARWMH(num_chains=C, **kw)
@@ -87,7 +87,7 @@ def test_pooled_blocks_bitexact(kind, d, C, blocks, K, gpu, orc):
 def test_pooled_blocks_inplace(d, C, K, gpu, orc):
     """sample_(12) with sync_every = K in place (amh_pooled_step_k) equals
     12 / K out-of-place block samples."""
-    from kernels import PooledARWMH, PRNGKey
+    from kernels_amd import PooledARWMH, PRNGKey
     kw, mk, om = make_case("gaussian", d)
     z0 = torch.empty(C, d, device=gpu).uniform_(-2, 2)
     a = PooledARWMH(num_chains=C, sync_every=K, **kw)
@@ -112,8 +112,8 @@ def _gpu_worker(rank, world, port, C, steps, out_path):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks share the box's one GPU
     import posteriors as P
-    from kernels import PooledARWMH, PRNGKey
-    from kernels.distributed import gather_chains, shard_range
+    from kernels_amd import PooledARWMH, PRNGKey
+    from kernels_amd.distributed import gather_chains, shard_range
     g = P.correlated_gaussian(32)
     off, cnt = shard_range(C, rank, world)
     z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, 32)).astype(np.float32))
@@ -134,7 +134,7 @@ def test_pooled_two_ranks(gpu, tmp_path):
     import socket
     import torch.multiprocessing as mp
     import posteriors as P
-    from kernels import PooledARWMH, PRNGKey
+    from kernels_amd import PooledARWMH, PRNGKey
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]

@@ -1,11 +1,11 @@
 """infer.diagnostics: known answers for the numpyro estimators restated in
-adaptive-mcmc_amd/infer/diagnostics.py (numpyro itself is not importable
+adaptive-mcmc_amd/infer_amd/diagnostics.py (numpyro itself is not importable
 here, so the definitions are pinned by closed forms and by a direct O(N^2)
 restatement of the same formulas)."""
 import numpy as np
 import pytest
 
-from infer import diagnostics as D
+from infer_amd import diagnostics as D
 
 
 def _ar1(rng, C, N, phi):

@@ -5,7 +5,7 @@ import numpy as np
 import pytest
 import torch
 
-from utils import lipschitz as Lz
+from utils_amd import lipschitz as Lz
 
 
 def test_spectral_norm_caps_sigma():
@@ -36,7 +36,7 @@ def test_contraction_and_kernel_distance_on_device(gpu):
     (f is 1-Lipschitz; Pf from 2e4 draws per point, pairs 0.2 apart); the
     kernel distance of P to itself (independent draws) is small."""
     import posteriors as P
-    from kernels import ARWMH, PRNGKey
+    from kernels_amd import ARWMH, PRNGKey
     g = P.gaussian(np.zeros(1), cov=np.eye(1))
     k = ARWMH(potential_fn=g, num_chains=1)
     adapt = k.get_init_adapt_state(PRNGKey(0), torch.zeros(1, 1))

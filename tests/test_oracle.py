@@ -19,7 +19,15 @@ TOL = dict(z=(1e-5, 1e-5), mu=(1e-5, 1e-5), pe=(2e-5, 1e-3), lam=(0, 3e-5), macc
 
 
 def lit_potential(kind, om):
-    d, data = om.d, np.asarray(om.data, np.float64)
+    d = om.d
+    if kind == "diamonds_ss":  # same posterior: the literal model reads the direct data
+        import posteriors as P
+        arr, (N, K) = P.diamonds.pack_fn(P.synthetic_diamonds(N=500))
+        arr = arr.astype(np.float64)
+        return lambda z: lit.diamonds_potential(z, arr[:N * (K - 1)].reshape(N, K - 1), arr[N * (K - 1):])
+    # (the diamonds_ss buffer holds float64 statistics as float32 word pairs,
+    # so it is never cast; the other models' data are plain float32)
+    data = np.asarray(om.data, np.float64)
     if kind == "gaussian":
         m, P, c0 = data[:d], data[d:d + d * d].reshape(d, d), data[d + d * d]
         return lambda z: lit.gaussian_potential(z, m, P, c0)
@@ -32,11 +40,6 @@ def lit_potential(kind, om):
     if kind == "diamonds":
         N, Kc = om.n_data, om.k_data - 1
         return lambda z: lit.diamonds_potential(z, data[:N * Kc].reshape(N, Kc), data[N * Kc:])
-    if kind == "diamonds_ss":  # same posterior: the literal model reads the direct data
-        import posteriors as P
-        arr, (N, K) = P.diamonds.pack_fn(P.synthetic_diamonds(N=500))
-        arr = arr.astype(np.float64)
-        return lambda z: lit.diamonds_potential(z, arr[:N * (K - 1)].reshape(N, K - 1), arr[N * (K - 1):])
     raise ValueError(kind)
 
 
@@ -91,7 +94,7 @@ def test_oracle_step_matches_literal(kind, dim, pre_steps, orc):
     """One teacher-forced transition (identical noise) of the C oracle against
     the literal float64 restatement; d = 128 / 256 exercise the large-d bit
     spec (wave-per-chain passes, MFMA-order potential)."""
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     _, _, om = make_case(kind, dim)
     d, C, W = om.d, (48 if om.d <= 64 else 12), 20
     st = orc.init(om, PRNGKey(3), C)
@@ -134,7 +137,7 @@ def test_frozen_kernel_stationary_acceptance(orc):
     """1-D N(0,1) target, frozen L = 1, lambda = 0 (asumptions_check.ipynb):
     stationary acceptance of RWM with proposal sd s is (2/pi) atan(2/s)."""
     import posteriors as P
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     g = P.gaussian(np.zeros(1), cov=np.eye(1))
     data, _ = g.pack("cpu")
     om = orc.Model(orc.GAUSSIAN, 1, data.numpy())
@@ -146,7 +149,7 @@ def test_frozen_kernel_stationary_acceptance(orc):
 
 
 def test_adaptation_reaches_target(orc):
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     _, _, om = make_case("gaussian", 8)
     st = orc.init(om, PRNGKey(0), 64)
     acc = np.zeros(64, np.int32)
@@ -165,7 +168,7 @@ def test_eight_schools_posterior(orc):
     """posteriordb_eight-schools.ipynb:858-867 (NumPyro summary of the
     reference ARWMH run): mu 4.40 (sd 3.29), tau 3.63 (sd 3.21),
     theta_base[0] 0.32 (sd 0.99)."""
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     _, _, om = make_case("eight_schools")
     C = 128
     st = orc.init(om, PRNGKey(11), C)
@@ -214,7 +217,7 @@ def test_diamonds_suffstat_same_chain_statistics(orc):
     chains sample the same posterior: mean acceptance agrees to 2e-3 (measured
     4e-5)."""
     import posteriors as P
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     mk = P.synthetic_diamonds()
     a, (N, K) = P.diamonds.pack_fn(mk)
     s, _ = P.diamonds_suffstat.pack_fn(mk)

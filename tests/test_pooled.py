@@ -1,4 +1,4 @@
-"""Pooled-covariance mode (regime B, kernels/pooled.py + orc_pooled_*) on
+"""Pooled-covariance mode (regime B, kernels_amd/pooled.py + orc_pooled_*) on
 the CPU: the oracle's pooled step with ONE chain reproduces the reference
 recurrence (golden vectors of the literal restatement), the pooled
 adaptation converges to the target covariance with many chains, and a
@@ -97,8 +97,8 @@ def _pooled_worker(rank, world, port, C, steps, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import orc
     from helpers import make_case
-    from kernels import PRNGKey
-    from kernels.distributed import gather_chains, shard_range
+    from kernels_amd import PRNGKey
+    from kernels_amd.distributed import gather_chains, shard_range
     _, _, om = make_case("gaussian", 12)
     off, cnt = shard_range(C, rank, world)
     st = orc.init(om, PRNGKey(9), cnt, chain_offset=off)
@@ -118,7 +118,7 @@ def _pooled_worker(rank, world, port, C, steps, out_path):
 
 def test_two_ranks_match_one(tmp_path, orc):
     from helpers import make_case
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     C, steps = 301, 40
     out = str(tmp_path / "p.npz")
     mp.start_processes(_pooled_worker, args=(2, _free_port(), C, steps, out), nprocs=2, join=True,
@@ -146,7 +146,7 @@ def test_one_chain_big_is_the_reference_recurrence(d, orc):
     gamma_1 = 1 keep-L quirk twice)."""
     import arwmh_np as lit
     import posteriors as P
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     g = P.correlated_gaussian(d)
     data, _ = g.pack("cpu")
     om = orc.Model(orc.GAUSSIAN, d, data.numpy())
@@ -190,7 +190,7 @@ def test_block_is_k_frozen_steps(kind, d, C, K, orc):
     up to association order (d <= 64: one float32 accumulator per wave over
     all K steps; d > 64: the per-step sums added in step order, exactly)."""
     from helpers import make_case
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     _, _, om = make_case(kind, d)
     st = orc.init(om, PRNGKey(3), C)
     z, pe, keys = st.z, st.potential_energy, st.rng_key
@@ -216,7 +216,7 @@ def test_block_update_counts_blocks(orc):
     """update_k: i advances by K; gamma = 1/n^a with n the block count
     (i / K + 1), reset at num_warmup; K = 1 is the per-step rule."""
     from helpers import make_case
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     K, W, C, a = 4, 8, 50, 2 / 3
     _, _, om = make_case("gaussian", 6)
     st = orc.init(om, PRNGKey(1), C)
@@ -245,8 +245,8 @@ def _pooled_block_worker(rank, world, port, C, steps, K, out_path):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     import orc
     from helpers import make_case
-    from kernels import PRNGKey
-    from kernels.distributed import gather_chains, shard_range
+    from kernels_amd import PRNGKey
+    from kernels_amd.distributed import gather_chains, shard_range
     _, _, om = make_case("gaussian", 12)
     off, cnt = shard_range(C, rank, world)
     st = orc.init(om, PRNGKey(9), cnt, chain_offset=off)
@@ -269,7 +269,7 @@ def test_two_ranks_match_one_blocks(tmp_path, orc):
     """sync_every = 4 over 2 gloo ranks (one all-reduce per block) equals the
     single-process block run up to the association order of the sums."""
     from helpers import make_case
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     C, steps, K = 301, 40, 4
     out = str(tmp_path / "pb.npz")
     mp.start_processes(_pooled_block_worker, args=(2, _free_port(), C, steps, K, out), nprocs=2, join=True,
@@ -290,7 +290,7 @@ def test_two_ranks_match_one_blocks(tmp_path, orc):
 
 
 def test_sync_every_argument_checks():
-    from kernels import PooledARWMH
+    from kernels_amd import PooledARWMH
     import posteriors as P
     with pytest.raises(ValueError):
         PooledARWMH(potential_fn=P.correlated_gaussian(4), num_chains=8, sync_every=0)

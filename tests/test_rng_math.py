@@ -30,7 +30,7 @@ def test_philox_kat_c(orc):
 
 
 def test_philox_kat_numpy_and_product():
-    from kernels import random as krandom
+    from kernels_amd import random as krandom
     for ctr, key, exp in KAT:
         o = lit.philox4x32_10(*[np.uint32(c) for c in ctr], np.uint32(key[0]), np.uint32(key[1]))
         assert tuple(int(v) for v in o) == exp

@@ -1,7 +1,7 @@
 """Driver helpers (reference python/utils/kernel_utils.py)."""
 import numpy as np
 
-from utils.kernel_utils import ns_logscale
+from utils_amd.kernel_utils import ns_logscale
 
 
 def test_ns_logscale_grid():

@@ -4,7 +4,7 @@ import os, sys, time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "adaptive-mcmc_amd"))
 import torch
 import posteriors as P
-from kernels import ARWMH, PRNGKey
+from kernels_amd import ARWMH, PRNGKey
 dev = torch.device("cuda", 0)
 C, d = 65536, 64
 k = ARWMH(potential_fn=P.correlated_gaussian(d), num_chains=C, device=dev)

@@ -36,7 +36,7 @@ def timed(fn, steps, stream):
 
 def run_regime_a(name, kernel, C, d, kwargs, steps, warmup, dev):
     import torch
-    from kernels import PRNGKey
+    from kernels_amd import PRNGKey
     gen = torch.Generator(device=dev)
     gen.manual_seed(7)
     z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
@@ -62,7 +62,7 @@ def main():
     args = ap.parse_args()
     import torch
     import posteriors as P
-    from kernels import ARWMH, ASSS, PooledARWMH, PRNGKey
+    from kernels_amd import ARWMH, ASSS, PooledARWMH, PRNGKey
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     want = set(args.only.split(","))

@@ -4,8 +4,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "adaptive-mcmc_amd"))
 import torch
 import posteriors as P
-from infer import MCMC
-from kernels import ARWMH, PRNGKey
+from infer_amd import MCMC
+from kernels_amd import ARWMH, PRNGKey
 dev = torch.device("cuda", 0)
 for C, W, N, th in [(64, 5000, 50000, 50), (64, 50000, 500000, 50), (1024, 50000, 500000, 50)]:
     k = ARWMH(model=P.eight_schools, num_chains=C, device=dev)

@@ -7,7 +7,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import torch  # noqa: E402
 
 import posteriors as P  # noqa: E402
-from kernels import PooledARWMH, PRNGKey  # noqa: E402
+from kernels_amd import PooledARWMH, PRNGKey  # noqa: E402
 
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 64

@@ -18,8 +18,8 @@ sys.path.insert(0, os.path.join(ROOT, "adaptive-mcmc_amd"))
 import torch  # noqa: E402
 
 import posteriors as P  # noqa: E402
-from kernels import ARWMH, PRNGKey  # noqa: E402
-from kernels import _lib  # noqa: E402
+from kernels_amd import ARWMH, PRNGKey  # noqa: E402
+from kernels_amd import _lib  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--chains", type=int, default=65536)
