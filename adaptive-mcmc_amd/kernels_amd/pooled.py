@@ -71,12 +71,30 @@ class PooledARWMH(ARWMH):
     (and, across ranks, the one all-reduce) cover the block's K * C
     chain-steps, and one update ends it, with gamma counting blocks.  Then
     `sample` advances one block and `sample_(n)` needs n % K == 0;
-    num_warmup must be a multiple of K."""
+    num_warmup must be a multiple of K.
+
+    The all-reduce runs on a side stream of its own (RCCL); the compute
+    stream waits on its event only where the sums are consumed.
+
+    overlap = True (the all-reduce overlapped with the next
+    proposal) pools with a lag of one block: block b+1 runs with the shared
+    state that block b-1's sums produced while block b's sums are still being
+    all-reduced, i.e.
+
+        theta_{b+1} = update(theta_b, sums_{b-1}),   theta_1 = theta_0,
+
+    with the noise position advancing every block as usual.  The update rule
+    is unchanged (delta measured from the mean of the block the sums come
+    from); only which sums it consumes differs, so this is a delayed
+    stochastic-approximation step.  The sums of the last block stay pending
+    in the sampler and are applied by the next call.  Results do not depend on
+    the rank count (up to the association order of the sums across ranks)."""
 
     pooled = True  # adapt-state leaves carry no chain axis
 
     def __init__(self, model=None, potential_fn=None, lr_decay=2 / 3, target_accept_prob=0.234, eps=1e-6,
-                 num_chains=None, device=None, chain_offset=0, group=None, sync_every: int = 1, **kw):
+                 num_chains=None, device=None, chain_offset=0, group=None, sync_every: int = 1,
+                 overlap: bool = False, **kw):
         super().__init__(model=model, potential_fn=potential_fn, lr_decay=lr_decay,
                          target_accept_prob=target_accept_prob, eps=eps, num_chains=num_chains, device=device,
                          chain_offset=chain_offset, **kw)
@@ -84,7 +102,11 @@ class PooledARWMH(ARWMH):
             raise ValueError("sync_every must be >= 1")
         self._group = group
         self._sums = None
+        self._bufs = None
+        self._pending = None  # overlap: (buffer index, all-reduce event or None) not yet applied
+        self._comm = None
         self.sync_every = int(sync_every)
+        self.overlap = bool(overlap)
 
     def _world(self) -> int:
         if not dist.is_available() or not dist.is_initialized():
@@ -104,7 +126,9 @@ class PooledARWMH(ARWMH):
         from .arwmh import pack_scale
         cov = pack_scale(eye)
         adapt = PooledAdaptState(torch.zeros(d, **f), cov.to(torch.float32), torch.zeros(1, **f))
-        self._sums = torch.zeros(sums_size(d), dtype=torch.float64, device=dev)
+        self._bufs = torch.zeros(2, sums_size(d), dtype=torch.float64, device=dev)
+        self._sums = self._bufs[0]
+        self._pending = None
         return PooledState(torch.zeros(1, dtype=torch.int32, device=dev), st.z, st.potential_energy,
                            torch.zeros(1, **f), adapt, torch.zeros(1, **f), st.rng_key, cov)
 
@@ -139,21 +163,72 @@ class PooledARWMH(ARWMH):
                                             torch.empty_like(a.log_step_size)),
                            torch.empty_like(s.as_change), s.rng_key, torch.empty_like(s.cov))
 
+    # ------------------------------------------------------- the exchange --
+    def _allreduce(self, buf: torch.Tensor, dev: int):
+        """all_reduce(sum) of one sums buffer.  RCCL: enqueued on the side
+        stream after the compute stream's work so far; returns the event the
+        consumer waits on.  gloo (ranks sharing a device, CPU tests): done
+        in place, host-synchronous; returns None."""
+        if self._world() == 1:
+            return None
+        if dist.get_backend(self._group) != "nccl":
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self._group)
+            return None
+        if self._comm is None:
+            self._comm = torch.cuda.Stream(device=dev)
+        self._comm.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(self._comm):
+            dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self._group)
+            ev = torch.cuda.Event()
+            ev.record(self._comm)
+        return ev
+
+    def _stats(self, L, cin, sout, buf, C):
+        dev = sout.z.device.index
+        _lib.check(L.amh_pooled_stats_k(self._handle.h, C, ctypes.byref(cin), self.sync_every, _lib.ptr(sout.z),
+                                        _lib.ptr(sout.potential_energy), _lib.ptr(buf), _lib.stream_ptr(dev)),
+                   self._handle.h)
+
+    def _update(self, L, buf, cin, cout):
+        dev = buf.device.index
+        _lib.check(L.amh_pooled_update_k(self._handle.h, _lib.ptr(buf), ctypes.byref(cin), ctypes.byref(cout),
+                                         self.sync_every, _lib.stream_ptr(dev)), self._handle.h)
+
     def _one(self, sin: PooledState, sout: PooledState):
         L = _bind_pooled(_lib.lib())
         dev = sin.z.device.index
         C = sin.z.shape[0]
         cin, cout = self._c(sin), self._c(sout)
-        K = self.sync_every
         with torch.cuda.device(dev):
-            stream = _lib.stream_ptr(dev)
-            _lib.check(L.amh_pooled_stats_k(self._handle.h, C, ctypes.byref(cin), K, _lib.ptr(sout.z),
-                                            _lib.ptr(sout.potential_energy), _lib.ptr(self._sums), stream),
-                       self._handle.h)
-            if self._world() > 1:
-                dist.all_reduce(self._sums, op=dist.ReduceOp.SUM, group=self._group)
-            _lib.check(L.amh_pooled_update_k(self._handle.h, _lib.ptr(self._sums), ctypes.byref(cin),
-                                             ctypes.byref(cout), K, stream), self._handle.h)
+            if not self.overlap:
+                buf = self._bufs[0]
+                self._stats(L, cin, sout, buf, C)
+                ev = self._allreduce(buf, dev)
+                if ev is not None:
+                    torch.cuda.current_stream(dev).wait_event(ev)
+                self._update(L, buf, cin, cout)
+                self._sums = buf
+                return
+            b = 0 if self._pending is None else 1 - self._pending[0]
+            buf = self._bufs[b]
+            self._stats(L, cin, sout, buf, C)
+            ev = self._allreduce(buf, dev)  # in flight while the next block computes
+            if self._pending is not None:
+                pb, pev = self._pending
+                if pev is not None:
+                    torch.cuda.current_stream(dev).wait_event(pev)
+                self._update(L, self._bufs[pb], cin, cout)
+            else:  # first block: theta_1 = theta_0, the noise position advances
+                if sout is not sin:
+                    for a, c in ((sin.adapt_state.loc, sout.adapt_state.loc),
+                                 (sin.adapt_state.scale, sout.adapt_state.scale),
+                                 (sin.adapt_state.log_step_size, sout.adapt_state.log_step_size),
+                                 (sin.mean_accept_prob, sout.mean_accept_prob), (sin.as_change, sout.as_change),
+                                 (sin.cov, sout.cov)):
+                        c.copy_(a)
+                torch.add(sin.i, self.sync_every, out=sout.i)
+            self._pending = (b, ev)
+            self._sums = buf
 
     def sample(self, state, model_args=(), model_kwargs=None):
         """One pooled transition of every chain (sync_every > 1: one block of
@@ -169,20 +244,48 @@ class PooledARWMH(ARWMH):
         K = self.sync_every
         if int(n_steps) % K != 0:
             raise ValueError(f"n_steps ({n_steps}) must be a multiple of sync_every ({K})")
-        if self._world() == 1:
+        if self._world() == 1 and not self.overlap:
             L = _bind_pooled(_lib.lib())
             dev = state.z.device.index
             c = self._c(state)
             with torch.cuda.device(dev):
                 _lib.check(L.amh_pooled_step_k(self._handle.h, C, ctypes.byref(c), ctypes.byref(c), int(n_steps), K,
-                                               _lib.ptr(self._sums), _lib.stream_ptr(dev)), self._handle.h)
+                                               _lib.ptr(self._bufs[0]), _lib.stream_ptr(dev)), self._handle.h)
+            self._sums = self._bufs[0]
             return state
         for _ in range(int(n_steps) // K):
             self._one(state, state)
         return state
 
-    def run(self, *a, **k):
-        raise NotImplementedError("pooled mode: use sample / sample_")
+    def run(self, state, n_steps: int, thinning: int = 1, collect_z: bool = True, collect_pe: bool = False):
+        """n_steps pooled transitions (numpyro fori_collect over sample):
+        returns (new_state, z [n_steps // thinning, C, d] or None, pe or None).
+        Draws are taken at block ends, so thinning must be a multiple of
+        sync_every (and n_steps of both)."""
+        C = self._check(state)
+        K = self.sync_every
+        if int(thinning) < 1 or int(thinning) % K != 0 or int(n_steps) % K != 0:
+            raise ValueError(f"thinning ({thinning}) and n_steps ({n_steps}) must be multiples of sync_every ({K})")
+        out = self._new_like(state)  # (shares the constant rng_key leaf)
+        for t, src in ((out.i, state.i), (out.z, state.z), (out.potential_energy, state.potential_energy),
+                       (out.mean_accept_prob, state.mean_accept_prob), (out.as_change, state.as_change),
+                       (out.cov, state.cov)) + tuple(zip(out.adapt_state, state.adapt_state)):
+            t.copy_(src)
+        keep = int(n_steps) // int(thinning)
+        dev = state.z.device
+        cz = torch.empty(keep, C, self._dim, dtype=torch.float32, device=dev) if collect_z and keep else None
+        cp = torch.empty(keep, C, dtype=torch.float32, device=dev) if collect_pe and keep else None
+        done = 0
+        for k in range(keep):
+            self.sample_(out, int(thinning))
+            done += int(thinning)
+            if cz is not None:
+                cz[k].copy_(out.z)
+            if cp is not None:
+                cp[k].copy_(out.potential_energy)
+        if int(n_steps) > done:
+            self.sample_(out, int(n_steps) - done)
+        return out, cz, cp
 
     def get_diagnostics_str(self, state):
         acc = float(state.mean_accept_prob[0])

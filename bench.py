@@ -1,21 +1,35 @@
-"""Headline benchmark: chain-steps/s of ARWMH.sample on the 64-d correlated
-Gaussian (BASELINE.json configs[1]: 65,536 chains per MI355X), plus ESS/s,
-roofline of the step kernel and the CPU baseline (C oracle, OpenMP).
+"""Headline benchmark (BASELINE.json): chain-steps/s of the whole node + ESS/s
+on the 64-d correlated Gaussian.
 
-A "step" is one ARWMH.sample transition of every chain: one launch of the
-step kernel that reads and writes the whole chain state in HBM (the
-sample() API contract).  Weak scaling: each rank owns 65,536 chains (global
-ids rank*C ...); chains are independent, so there is no collective in the
-timed region.
+A "step" is one transition of every chain.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--chains C] [--dim D]
-  N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+N = 1 (BASELINE configs[1]): ARWMH.sample, per-chain adaptation (the
+  reference's semantics, arwmh.py:140-207), 65,536 chains: one launch of the
+  step kernel per step, reading and writing the whole chain state in HBM (the
+  sample() API contract).  Roofline: HBM, B_A(64) = 17,712 B per chain-step.
+N > 1 (BASELINE configs[4]): pooled-covariance ARWMH, 65,536 chains per GPU
+  (weak scaling), all-reduce(sum) of the pooled sums over RCCL every step and
+  a shared refactorisation on every rank (kernels_amd/pooled.py).  Sub-fields:
+  the same with pooling every 16 steps, with the all-reduce overlapped
+  (lag-one pooling), the strong-scaling forms (524,288 chains in total), and
+  regime A (no collective).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset) the script
+starts its N ranks itself, as child processes, before anything touches a
+GPU; under torch.distributed.run it is one of the launched ranks.  Every rank
+asserts WORLD_SIZE == --gpus.  When fewer GPUs are visible than ranks (the
+1-GPU test box), the ranks share the devices and exchange over gloo; the line
+then says so in config.parallelism.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -27,11 +41,19 @@ for _p in (os.path.join(ROOT, "adaptive-mcmc_amd"), ROOT):
         sys.path.insert(0, _p)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector = FP32 matrix (dense)
+CONFIG5_TOTAL = 524288  # BASELINE configs[4]: 8 x 65,536 chains
 
 
 def bytes_per_chain_step(d: int) -> int:
     """SURVEY.md §8(d) B_A(d): state round trip, packed factor."""
     return 2 * 4 * (d * (d + 1) // 2 + 2 * d + 6)
+
+
+def pooled_flops_per_chain_step(d: int) -> int:
+    """SURVEY.md §8(d) regime B: proposal L xi (d(d+1)/2 FMA), the quadratic
+    form of the potential (d^2 FMA), the outer-product sum (d(d+1)/2 FMA)."""
+    return 2 * (d * (d + 1) // 2 + d * d + d * (d + 1) // 2)
 
 
 def ess_of(x: np.ndarray) -> float:
@@ -57,39 +79,211 @@ def measured_traffic(C: int, d: int):
     return best
 
 
-def bench_pooled(g, C: int, dev, rank: int, world: int, steps: int, warmup: int, sync_every: int = 1):
-    """Regime B (pooled covariance, BASELINE.json configs[4] at N = 8): every
-    step = per-chain transition + local sums, all-reduce(sum) of the sums over
-    RCCL (world > 1), shared refactorisation on every rank.  sync_every = K:
-    one all-reduce and refactorisation per K transitions."""
-    import torch
-    import torch.distributed as dist
-    from kernels_amd import PooledARWMH, PRNGKey
-    K = sync_every
-    steps, warmup = -(-steps // K) * K, -(-warmup // K) * K
-    k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=rank * C, sync_every=K)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(99 + rank)
-    z0 = (torch.rand(C, g.dim, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
-    st = k.init(PRNGKey(0), 0, z0, (), {})
-    k.sample_(st, warmup)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    k.sample_(st, steps)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([wall], dtype=torch.float64, device=dev)
+# ----------------------------------------------------------------- ranks --
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn_ranks(n: int) -> int:
+    """Start n ranks of this script (no GPU call in this process) and return
+    the first non-zero exit code; if one rank fails the others are stopped."""
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        if self.world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={self.world}")
+        self.rank = int(os.environ.get("RANK", "0"))
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        ndev = torch.cuda.device_count()  # does not initialise the GPU
+        if ndev < 1:
+            raise SystemExit("bench.py: no GPU visible")
+        self.ndev = ndev
+        self.shared = ndev < self.world
+        self.dev_index = local % ndev
+        self.backend = None
+        if self.world > 1:
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            self.backend = "gloo" if self.shared else "nccl"
+            torch.cuda.set_device(self.dev_index)
+            if self.backend == "nccl":
+                dist.init_process_group("nccl", device_id=torch.device("cuda", self.dev_index))
+            else:
+                dist.init_process_group("gloo")
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+
+    def barrier(self):
+        import torch.distributed as dist
+        if self.world > 1:
+            dist.barrier()
+
+    def max_over_ranks(self, x: float) -> float:
+        import torch
+        import torch.distributed as dist
+        if self.world == 1:
+            return float(x)
+        t = torch.tensor([float(x)], dtype=torch.float64)
+        if self.backend == "nccl":
+            t = t.to(self.dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        wall = float(t.item())
-    return {"value": world * C * steps / wall, "unit": "chain-steps/s", "ms_per_step": wall / steps * 1e3,
-            "steps": steps, "chains_per_gpu": C, "allreduce_doubles": g.dim + g.dim * (g.dim + 1) // 2 + 2,
-            "mean_accept_prob": float(st.mean_accept_prob[0]), "sync_every": K,
-            "collective": (f"all_reduce(sum) per {K} step(s)" if world > 1 else "none (1 rank)")}
+        return float(t.item())
+
+    def parallelism(self, what: str) -> str:
+        if self.world == 1:
+            return what
+        if self.shared:
+            return f"{what}; {self.world} ranks sharing {self.ndev} GPU(s), gloo exchange (test box)"
+        return f"{what}; {self.world} ranks, one per GPU, RCCL"
+
+
+def timed_region(ctx, fn):
+    """barrier + synchronize on both sides of `fn()`, max wall over ranks."""
+    import torch
+    torch.cuda.synchronize()
+    ctx.barrier()
+    t0 = time.perf_counter()
+    fn()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    return ctx.max_over_ranks(time.perf_counter() - t0)
+
+
+# ------------------------------------------------------------------- legs --
+def leg_regime_a(ctx, g, C, off, steps, warmup):
+    """ARWMH.sample per step (per-chain adaptation); HIP events on the launch
+    stream bracket the step launches only."""
+    import torch
+    from kernels_amd import ARWMH, PRNGKey
+    d = g.dim
+    k = ARWMH(potential_fn=g, num_chains=C, device=ctx.dev, chain_offset=off)
+    gen = torch.Generator(device=ctx.dev)
+    gen.manual_seed(1234 + ctx.rank)
+    z0 = (torch.rand(C, d, device=ctx.dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = k.init(PRNGKey(0), 0, z0, (), {})
+    for _ in range(warmup):
+        k.sample_(st, 1)
+    stream = torch.cuda.current_stream(ctx.dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+
+    def run():
+        ev0.record(stream)
+        for _ in range(steps):
+            k.sample_(st, 1)  # one full-state round trip per step (sample() semantics)
+        ev1.record(stream)
+
+    wall = timed_region(ctx, run)
+    kern_ms = ev0.elapsed_time(ev1) / steps
+    return dict(wall=wall, kern_ms=kern_ms, kernel=k, state=st)
+
+
+def leg_pooled(ctx, g, C, off, steps, warmup, K=1, overlap=False, burn_in=0):
+    """Regime B (pooled covariance): per-chain transitions with the shared
+    state, all-reduce(sum) of the sums over the ranks, shared update.  The
+    adaptation burns in for `burn_in` untimed steps before the warmup."""
+    import torch
+    from kernels_amd import PooledARWMH, PRNGKey
+    steps, warmup, burn_in = (-(-x // K) * K for x in (steps, warmup, burn_in))
+    k = PooledARWMH(potential_fn=g, num_chains=C, device=ctx.dev, chain_offset=off, sync_every=K,
+                    overlap=overlap)
+    gen = torch.Generator(device=ctx.dev)
+    gen.manual_seed(99 + ctx.rank)
+    z0 = (torch.rand(C, g.dim, device=ctx.dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = k.init(PRNGKey(0), 0, z0, (), {})
+    k.sample_(st, burn_in + warmup)
+    wall = timed_region(ctx, lambda: k.sample_(st, steps))
+    return dict(wall=wall, steps=steps, kernel=k, state=st, burn_in=burn_in, warmup=warmup)
+
+
+def pooled_stats_ms(k, st, C, reps=20):
+    """HIP-event time of the dominant pooled kernel (per-chain transitions +
+    chunk sums, amh_pooled_stats_k) alone, on the launch stream."""
+    import ctypes
+    import torch
+    from kernels_amd import _lib
+    from kernels_amd.pooled import _bind_pooled
+    L = _bind_pooled(_lib.lib())
+    dev = st.z.device.index
+    c = k._c(st)
+    zt, pt = torch.empty_like(st.z), torch.empty_like(st.potential_energy)
+    sums = torch.empty_like(k._bufs[0])
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(reps + 2):
+        if r == 2:
+            ev0.record(stream)
+        _lib.check(L.amh_pooled_stats_k(k._handle.h, C, ctypes.byref(c), k.sync_every, _lib.ptr(zt), _lib.ptr(pt),
+                                        _lib.ptr(sums), _lib.stream_ptr(dev)), k._handle.h)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return ev0.elapsed_time(ev1) / reps
+
+
+def pooled_line(ctx, r, total, d, C):
+    k = r["kernel"]
+    K = k.sync_every
+    st = r["state"]
+    coll = "none (1 rank)"
+    if ctx.world > 1:
+        coll = f"all_reduce(sum) per {K} step(s)" + (", lag-one overlap" if k.overlap else "")
+    return {"value": total * r["steps"] / r["wall"], "unit": "chain-steps/s",
+            "ms_per_step": r["wall"] / r["steps"] * 1e3, "steps": r["steps"], "chains_per_gpu": C,
+            "chains_total": total, "sync_every": K, "overlap": bool(k.overlap), "burn_in": r["burn_in"],
+            "mean_accept_prob": float(st.mean_accept_prob[0]), "allreduce_doubles": d + d * (d + 1) // 2 + 2,
+            "collective": coll}
+
+
+def ess_leg(ctx, g, burn_in=20000, T=1000, Cs=4096):
+    """ESS/s after a stated per-chain adaptation: Cs chains adapt for burn_in
+    steps (fused launches), then T recorded steps; ESS over 4 coordinates + U."""
+    import torch
+    from kernels_amd import ARWMH, PRNGKey
+    d = g.dim
+    ks = ARWMH(potential_fn=g, num_chains=Cs, device=ctx.dev)
+    gen = torch.Generator(device=ctx.dev)
+    gen.manual_seed(7)
+    zs = (torch.rand(Cs, d, device=ctx.dev, generator=gen) * 4.0 - 2.0).contiguous()
+    ss = ks.init(PRNGKey(1), 0, zs, (), {})
+    for _ in range(burn_in // 1000):
+        ks.sample_(ss, 1000)
+    torch.cuda.synchronize()
+    acc_burn = float(ss.mean_accept_prob.mean())
+    e0 = time.perf_counter()
+    ss, cz, cp = ks.run(ss, T, collect_z=True, collect_pe=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - e0
+    zc, pc = cz.cpu().numpy(), cp.cpu().numpy()
+    vals = [ess_of(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
+    vals.append(ess_of(pc.T.astype(np.float64)))
+    return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T, "seconds": el,
+            "burn_in": burn_in, "mean_accept_prob_after_burn_in": acc_burn,
+            "mean_accept_prob_window": float(ss.mean_accept_prob.mean()), "coords": [0, 1, d // 2, d - 1, "U"]}
 
 
 def cpu_baseline(g, d: int, budget_s: float = 12.0):
@@ -116,151 +310,114 @@ def cpu_baseline(g, d: int, budget_s: float = 12.0):
             "sample": f"C oracle (oracle/amh_oracle.c), {C} chains x {steps} steps, d={d}, {el:.1f} s"}
 
 
+# ------------------------------------------------------------------- main --
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--chains", type=int, default=65536, help="chains per GPU (weak scaling)")
-    ap.add_argument("--total-chains", type=int, default=0,
-                    help="strong scaling: this many chains split over the ranks (SURVEY.md §8(d) config 5: 524288)")
     ap.add_argument("--dim", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-ess", action="store_true")
-    ap.add_argument("--no-pooled", action="store_true")
+    ap.add_argument("--no-pooled", action="store_true", help="N = 1: skip the pooled sub-fields")
+    ap.add_argument("--no-extra", action="store_true", help="headline leg only (profiling runs)")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused 50-step launch (profiling runs)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args.gpus))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
-
+    ctx = Ctx(args)
     import posteriors as P
-    from kernels_amd import ARWMH, PRNGKey
-
     from kernels_amd.distributed import shard_range
     d, C = args.dim, args.chains
-    off = rank * C
-    strong = args.total_chains > 0
-    if strong:
-        off, C = shard_range(args.total_chains, rank, world)
+    world, rank = ctx.world, ctx.rank
     g = P.correlated_gaussian(d)
-    k = ARWMH(potential_fn=g, num_chains=C, device=dev, chain_offset=off)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(1234 + rank)
-    z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
-    st = k.init(PRNGKey(0), 0, z0, (), {})
+    extra = not args.no_extra
+    data = "synthetic (64-d correlated Gaussian, kappa=1e2, default_rng(64) rotation)"
+    metric = "chain-steps/sec (whole node) + ESS/sec, 64-dim Gaussian"
 
-    # untimed warmup (also burns in the adaptation)
-    for _ in range(args.warmup):
-        k.sample_(st, 1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    if world == 1:
+        # ---- headline: configs[1], regime A
+        r = leg_regime_a(ctx, g, C, 0, args.steps, args.warmup)
+        value = C * args.steps / r["wall"]
+        per_launch_bytes = C * bytes_per_chain_step(d)
+        achieved = per_launch_bytes / (r["kern_ms"] * 1e-3) / 1e9
+        traffic = measured_traffic(C, d)
+        roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
+                    "traffic_source": traffic[1] if traffic else None, "kernel_ms": r["kern_ms"],
+                    "kernel": "arwmh_step_kernel<64,GaussianM,true,0>",
+                    "algorithmic_bytes_per_launch": per_launch_bytes}
+        fused = None
+        if extra and not args.no_fused:
+            k, st = r["kernel"], r["state"]
+            torch.cuda.synchronize()
+            f0 = time.perf_counter()
+            k.sample_(st, 50)
+            torch.cuda.synchronize()
+            fused = C * 50 / (time.perf_counter() - f0)
+        sub = {}
+        if extra and not args.no_pooled:
+            for name, K, ov in (("pooled", 1, False), ("pooled_sync_every_16", 16, False),
+                                ("pooled_overlap", 1, True)):
+                pr = leg_pooled(ctx, g, C, 0, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
+                sub[name] = pooled_line(ctx, pr, C, d, C)
+        ess = ess_leg(ctx, g) if extra and not args.no_ess else None
+        cpu = cpu_baseline(g, d) if extra and not args.no_cpu_baseline else None
+        line = {"metric": metric, "value": value, "unit": "chain-steps/s", "n_gpus": 1, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": r["wall"] / args.steps * 1e3, "higher_is_better": True,
+                "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data,
+                "config": {"workload": (f"ARWMH.sample, d={d} correlated Gaussian, {C} chains, per-chain "
+                                        f"adaptation (BASELINE.json configs[1])"),
+                           "chains_per_gpu": C, "dim": d, "parallelism": "1 GPU"},
+                "roofline": roofline, "cpu_baseline": cpu, "ess": ess, "fused_chain_steps_per_s": fused, **sub}
+        print(json.dumps(line), flush=True)
+        return
 
-    stream = torch.cuda.current_stream(dev)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        k.sample_(st, 1)  # one full-state round trip per step (sample() semantics)
-    ev1.record(stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    wall = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # events bracket only step launches on this stream
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
-
-    total = args.total_chains if strong else world * C
-    value = total * args.steps / wall
-    per_launch_bytes = C * bytes_per_chain_step(d)
-    achieved_gbs = per_launch_bytes / (kern_ms * 1e-3) / 1e9
-
-    # fused multi-step launch (numpyro fori_collect semantics, state on chip)
-    fused_rate = None
-    if not args.no_fused:
-        fused_steps = 50
-        torch.cuda.synchronize()
-        f0 = time.perf_counter()
-        k.sample_(st, fused_steps)
-        torch.cuda.synchronize()
-        fused_rate = C * fused_steps / (time.perf_counter() - f0)
-
-    ess = None
-    if not args.no_ess and rank == 0:
-        # ESS/s: 1,000 recorded post-warmup steps of 4,096 chains (4 coordinates + U)
-        T, Cs = 1000, 4096
-        ks = ARWMH(potential_fn=g, num_chains=Cs, device=dev)
-        zs = (torch.rand(Cs, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
-        ss = ks.init(PRNGKey(1), 0, zs, (), {})
-        ks.sample_(ss, 2000)  # adaptation burn-in
-        torch.cuda.synchronize()
-        e0 = time.perf_counter()
-        ss, cz, cp = ks.run(ss, T, collect_z=True, collect_pe=True)
-        torch.cuda.synchronize()
-        el = time.perf_counter() - e0
-        zc = cz.cpu().numpy()
-        pc = cp.cpu().numpy()
-        vals = [ess_of(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
-        vals.append(ess_of(pc.T.astype(np.float64)))
-        ess = {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T,
-               "seconds": el, "coords": [0, 1, d // 2, d - 1, "U"]}
-
-    pooled = None
-    if not args.no_pooled:
-        pooled = bench_pooled(g, C, dev, rank, world, steps=max(args.steps, 20), warmup=5)
-        pooled["sync_every_16"] = bench_pooled(g, C, dev, rank, world, steps=max(args.steps, 32), warmup=16,
-                                               sync_every=16)
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(g, d)
-
-    traffic = measured_traffic(C, d)
+    # ---- N > 1 headline: configs[4], pooled all-reduce every step, weak
+    r = leg_pooled(ctx, g, C, rank * C, args.steps, args.warmup, K=1, burn_in=256)
+    total = world * C
+    head = pooled_line(ctx, r, total, d, C)
+    stats_ms = pooled_stats_ms(r["kernel"], r["state"], C)
+    flops = C * pooled_flops_per_chain_step(d)
+    achieved = flops / (stats_ms * 1e-3) / 1e12
+    roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel_ms": stats_ms,
+                "kernel": "pooled stats (amh_pooled_stats_k: transitions + chunk sums)",
+                "algorithmic_flops_per_launch": flops}
+    sub = {}
+    if extra:
+        for name, K, ov, strong in (("pooled_sync_every_16", 16, False, False), ("pooled_overlap", 1, True, False),
+                                    ("strong_pooled", 1, False, True), ("strong_pooled_sync_every_16", 16, False, True)):
+            if strong:
+                off, cnt = shard_range(CONFIG5_TOTAL, rank, world)
+                pr = leg_pooled(ctx, g, cnt, off, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
+                sub[name] = pooled_line(ctx, pr, CONFIG5_TOTAL, d, cnt)
+                sub[name]["scaling"] = "strong"
+            else:
+                pr = leg_pooled(ctx, g, C, rank * C, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
+                sub[name] = pooled_line(ctx, pr, total, d, C)
+        ra = leg_regime_a(ctx, g, C, rank * C, args.steps, args.warmup)
+        sub["regime_a"] = {"value": total * args.steps / ra["wall"], "unit": "chain-steps/s",
+                           "ms_per_step": ra["wall"] / args.steps * 1e3, "kernel_ms": ra["kern_ms"],
+                           "collective": "none (chains independent, BASELINE configs[1] per GPU)"}
     if rank == 0:
-        line = {
-            "metric": "chain-steps/sec (whole node) + ESS/sec, 64-dim Gaussian",
-            "value": value,
-            "unit": "chain-steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": wall / args.steps * 1e3,
-            "higher_is_better": True,
-            "scaling": "strong" if strong else "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (64-d correlated Gaussian, kappa=1e2, default_rng(64) rotation)",
-            "config": {"workload": f"ARWMH.sample, d={d} correlated Gaussian, "
-                                   + (f"{total} chains in total" if strong else f"{C} chains per GPU")
-                                   + ", per-chain adaptation (BASELINE.json configs[1])",
-                       "chains_per_gpu": C, "dim": d, "parallelism": f"chains sharded x{world}, no collective"},
-            "roofline": {"bound": "hbm", "achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved_gbs / HBM_PEAK_GBS,
-                         "traffic": traffic[0] if traffic else None,
-                         "traffic_source": traffic[1] if traffic else None,
-                         "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": per_launch_bytes},
-            "cpu_baseline": cpu,
-            "ess": ess,
-            "fused_chain_steps_per_s": fused_rate * total / C if fused_rate else None,
-            "pooled": pooled,
-        }
-        print(json.dumps(line))
-    if world > 1:
-        dist.destroy_process_group()
+        line = {"metric": metric, "value": head["value"], "unit": "chain-steps/s", "n_gpus": world,
+                "steps": head["steps"], "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
+                "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32", "data": data,
+                "config": {"workload": (f"pooled-covariance ARWMH, d={d} correlated Gaussian, {C} chains per GPU "
+                                        f"({total} in total), all_reduce(sum) of the pooled sums every step "
+                                        f"(BASELINE.json configs[4])"),
+                           "chains_per_gpu": C, "dim": d, "parallelism": ctx.parallelism(f"chains sharded x{world}")},
+                "roofline": roofline, "cpu_baseline": None, "pooled": head, **sub}
+        print(json.dumps(line), flush=True)
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -1,0 +1,27 @@
+"""bench.py's rank handling (CPU): a rank whose launcher world size does not
+match --gpus refuses to run, and the self-spawn path hands every child the
+launcher environment (the children fail cleanly here, with no GPU)."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(args, env_extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra)
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
+                          timeout=300, env=env)
+
+
+def test_world_mismatch_refused():
+    r = _run(["--gpus", "3"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
+    assert "--gpus 3 but WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def test_self_spawn_starts_n_ranks():
+    r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-extra"], {})
+    assert r.returncode != 0  # no GPU in this container: every rank stops at the device check
+    assert (r.stderr + r.stdout).count("no GPU visible") == 2

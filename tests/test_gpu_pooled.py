@@ -105,19 +105,87 @@ def test_pooled_blocks_inplace(d, C, K, gpu, orc):
         a.sample_(sa, 5 if K != 5 else 7)
 
 
-def _gpu_worker(rank, world, port, C, steps, out_path):
+@pytest.mark.parametrize("kind,d,C,blocks,K", [("gaussian", 64, 3000, 5, 1), ("gaussian", 64, 2000, 4, 4),
+                                               ("eight_schools", None, 64, 5, 2), ("gaussian", 128, 300, 3, 1)])
+def test_pooled_overlap_bitexact(kind, d, C, blocks, K, gpu, orc):
+    """overlap = True (lag-one pooling, the all-reduce in flight while the next
+    block computes): theta_{b+1} = update(theta_b, sums_{b-1}), theta_1 =
+    theta_0, bit for bit against the oracle's stats / update in that order;
+    the last block's sums stay pending and are applied by the next call."""
+    from kernels_amd import PooledARWMH, PRNGKey
+    kw, mk, om = make_case(kind, d)
+    k = PooledARWMH(num_chains=C, sync_every=K, overlap=True, **kw)
+    z0 = np.random.default_rng(3).uniform(-2, 2, size=(C, om.d)).astype(np.float32)
+    st = k.init(PRNGKey(3), 0, torch.as_tensor(z0), (), mk)
+    ost = orc.init(om, PRNGKey(3), C, init_z=z0)
+    z, pe, keys = ost.z, ost.potential_energy, ost.rng_key
+    sh = orc.pooled_init_shared(om.d)
+    pending = None
+    for b in range(blocks):
+        st = k.sample(st) if b % 2 == 0 else k.sample_(st, K)
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
+        if pending is None:
+            sh["i"] += K
+        else:
+            orc.pooled_update(om, pending, sh, k_steps=K)
+        pending = sums
+        torch.cuda.synchronize()
+        got = dict(z=st.z, pe=st.potential_energy, mu=st.adapt_state.loc, L=st.adapt_state.scale,
+                   lam=st.adapt_state.log_step_size, macc=st.mean_accept_prob, cov=st.cov, i=st.i)
+        want = dict(z=z, pe=pe, mu=sh["mu"], L=sh["L"], lam=sh["lam"], macc=sh["macc"], cov=sh["cov"], i=sh["i"])
+        for f in got:
+            a_, b_ = got[f].cpu().numpy(), np.asarray(want[f])
+            assert a_.tobytes() == b_.astype(a_.dtype).tobytes(), f"{kind} {f} differs at block {b + 1}"
+    # run() (draws at block ends) continues the same recurrence
+    st2, cz, cp = k.run(st, 2 * K, thinning=K, collect_z=True, collect_pe=True)
+    for t in range(2):
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
+        orc.pooled_update(om, pending, sh, k_steps=K)
+        pending = sums
+        torch.cuda.synchronize()
+        assert cz[t].cpu().numpy().tobytes() == z.tobytes() and cp[t].cpu().numpy().tobytes() == pe.tobytes()
+    assert st2.adapt_state.scale.cpu().numpy().tobytes() == sh["L"].tobytes()
+
+
+def test_pooled_run_matches_sample(gpu):
+    """PooledARWMH.run (collect at block ends) equals sample_ block by block."""
+    import posteriors as P
+    from kernels_amd import PooledARWMH, PRNGKey
+    g = P.correlated_gaussian(16)
+    z0 = torch.empty(500, 16, device=gpu).uniform_(-2, 2)
+    a = PooledARWMH(potential_fn=g, num_chains=500, sync_every=2)
+    sa = a.init(PRNGKey(1), 0, z0, (), {})
+    b = PooledARWMH(potential_fn=g, num_chains=500, sync_every=2)
+    sb = b.init(PRNGKey(1), 0, z0, (), {})
+    out, cz, cp = a.run(sa, 13 * 2, thinning=4, collect_z=True, collect_pe=True)
+    assert cz.shape == (6, 500, 16) and cp.shape == (6, 500)
+    for t in range(6):
+        b.sample_(sb, 4)
+        assert torch.equal(cz[t], sb.z) and torch.equal(cp[t], sb.potential_energy)
+    b.sample_(sb, 2)
+    torch.cuda.synchronize()
+    assert torch.equal(out.z, sb.z) and torch.equal(out.adapt_state.scale, sb.adapt_state.scale)
+    assert int(out.i[0]) == 26 and int(sa.i[0]) == 0  # run() leaves its input alone
+    with pytest.raises(ValueError):
+        a.run(sa, 4, thinning=3)
+
+
+def _gpu_worker(rank, world, port, C, steps, out_path, d=32, K=1, overlap=False):
     import os
     import torch
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)  # two ranks share the box's one GPU
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # the ranks share the box's one GPU
     import posteriors as P
     from kernels_amd import PooledARWMH, PRNGKey
     from kernels_amd.distributed import gather_chains, shard_range
-    g = P.correlated_gaussian(32)
+    g = P.correlated_gaussian(d)
     off, cnt = shard_range(C, rank, world)
-    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, 32)).astype(np.float32))
-    k = PooledARWMH(potential_fn=g, num_chains=cnt, chain_offset=off, device=torch.device("cuda", 0))
+    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, d)).astype(np.float32))
+    k = PooledARWMH(potential_fn=g, num_chains=cnt, chain_offset=off, device=torch.device("cuda", 0),
+                    sync_every=K, overlap=overlap)
     st = k.init(PRNGKey(2), 0, z0[off:off + cnt].cuda(), (), {})
     k.sample_(st, steps)
     z = gather_chains(st.z.cpu(), C)
@@ -127,10 +195,14 @@ def _gpu_worker(rank, world, port, C, steps, out_path):
     dist.destroy_process_group()
 
 
-def test_pooled_two_ranks(gpu, tmp_path):
+@pytest.mark.parametrize("d,C,steps,K,overlap,world", [(32, 2001, 25, 1, False, 2), (64, 3001, 12, 1, False, 2),
+                                                       (64, 3001, 16, 4, False, 3), (64, 2001, 12, 1, True, 2),
+                                                       (64, 2001, 16, 4, True, 2)])
+def test_pooled_two_ranks(d, C, steps, K, overlap, world, gpu, tmp_path):
     """The distributed path of PooledARWMH (all-reduce of the sums every
-    step) over 2 ranks equals the 1-rank run up to the association order of
-    the sums."""
+    block; with overlap, lag-one pooling) over several ranks equals the
+    1-rank run up to the association order of the sums (BASELINE config 5's
+    d = 64 workload, at test size)."""
     import socket
     import torch.multiprocessing as mp
     import posteriors as P
@@ -139,15 +211,18 @@ def test_pooled_two_ranks(gpu, tmp_path):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    C, steps = 2001, 25
     out = str(tmp_path / "g.npz")
-    mp.start_processes(_gpu_worker, args=(2, port, C, steps, out), nprocs=2, join=True, start_method="spawn")
+    mp.start_processes(_gpu_worker, args=(world, port, C, steps, out, d, K, overlap), nprocs=world, join=True,
+                       start_method="spawn")
     r = np.load(out)
-    g = P.correlated_gaussian(32)
-    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, 32)).astype(np.float32))
-    k = PooledARWMH(potential_fn=g, num_chains=C)
+    g = P.correlated_gaussian(d)
+    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(C, d)).astype(np.float32))
+    k = PooledARWMH(potential_fn=g, num_chains=C, sync_every=K, overlap=overlap)
     st = k.init(PRNGKey(2), 0, z0.to(gpu), (), {})
     k.sample_(st, steps)
     assert int(r["i"][0]) == steps
     np.testing.assert_allclose(r["L"], st.adapt_state.scale.cpu().numpy(), rtol=1e-4, atol=1e-5)
-    np.testing.assert_allclose(r["z"], st.z.cpu().numpy(), rtol=1e-4, atol=1e-4)
+    # a chain whose u sits within rounding of alpha may decide differently
+    # under the other association order; allow a handful of such chains
+    zd = np.abs(r["z"] - st.z.cpu().numpy()).max(axis=1) > 1e-4 * (1 + np.abs(r["z"]).max(axis=1))
+    assert zd.sum() <= max(2, C // 1000), zd.sum()
