@@ -465,6 +465,15 @@ int amh_pairwise_dist2(const float* a, int64_t n, const float* b, int64_t m, int
   return AMH_OK;
 }
 
+int amh_sinkhorn_lse(const float* cost, int64_t rows, int64_t cols, const float* pot, float log_w, float eps,
+                     float* out, void* stream) {
+  if (!cost || !pot || !out || rows < 1 || cols < 1 || !(eps > 0.0f) || rows > 0x7FFFFFFF)
+    return fail(nullptr, AMH_EINVAL, "amh_sinkhorn_lse: bad arguments");
+  const hipError_t e = amh::run_lse_rows(cost, rows, cols, pot, log_w, eps, out, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(nullptr, e, "amh_sinkhorn_lse");
+  return AMH_OK;
+}
+
 int amh_normals(const uint32_t key[2], int64_t n, float* out, void* stream) {
   if (!key || !out || n < 0) return fail(nullptr, AMH_EINVAL, "amh_normals: bad arguments");
   if (n == 0) return AMH_OK;

@@ -153,4 +153,60 @@ hipError_t run_dist2(const float* A, int64_t n, const float* B, int64_t m, int d
   return hipGetLastError();
 }
 
+// ------------------------------------------------------------- Sinkhorn --
+// One half-iteration of log-domain Sinkhorn (the solver behind the
+// reference's wasserstein_sinkhorn, evaluation.py:69-101, ott-jax
+// linear.solve): for every row i of the cost matrix C [rows][cols]
+//   out_i = -eps * log sum_j exp((pot_j - C_ij) / eps + log_w)
+// (uniform weights w = 1 / cols).  One 256-thread block per row streams the
+// row once (coalesced) with a running (max, sum) per thread, then combines the
+// pairs across the block.  The column half runs on the transposed matrix.
+// Bound: HBM (4 bytes of C per element, one exp each).
+__global__ __launch_bounds__(256) void lse_rows_kernel(const float* __restrict__ Cm, int64_t rows, int64_t cols,
+                                                       const float* __restrict__ pot, float logw, float eps,
+                                                       float* __restrict__ out) {
+  const int64_t i = blockIdx.x;
+  if (i >= rows) return;
+  const float* row = Cm + i * cols;
+  float mx = -INFINITY, sm = 0.0f;
+  for (int64_t j = threadIdx.x; j < cols; j += 256) {
+    const float a = (pot[j] - row[j]) / eps + logw;
+    if (a > mx) {
+      sm = sm * expf(mx - a) + 1.0f;
+      mx = a;
+    } else {
+      sm += expf(a - mx);
+    }
+  }
+  // combine (max, sum) pairs: lanes of the wave, then the four waves
+  for (int off = 32; off >= 1; off >>= 1) {
+    const float om = __shfl_xor(mx, off, 64);
+    const float os = __shfl_xor(sm, off, 64);
+    const float nm = fmaxf(mx, om);
+    sm = (nm == -INFINITY) ? 0.0f : sm * expf(mx - nm) + os * expf(om - nm);
+    mx = nm;
+  }
+  __shared__ float wm[4], wsum[4];
+  if ((threadIdx.x & 63) == 0) {
+    wm[threadIdx.x >> 6] = mx;
+    wsum[threadIdx.x >> 6] = sm;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float M = wm[0], S = wsum[0];
+    for (int k = 1; k < 4; ++k) {
+      const float nm = fmaxf(M, wm[k]);
+      S = (nm == -INFINITY) ? 0.0f : S * expf(M - nm) + wsum[k] * expf(wm[k] - nm);
+      M = nm;
+    }
+    out[i] = -eps * (M + logf(S));
+  }
+}
+
+hipError_t run_lse_rows(const float* Cm, int64_t rows, int64_t cols, const float* pot, float logw, float eps,
+                        float* out, hipStream_t s) {
+  hipLaunchKernelGGL(lse_rows_kernel, dim3((unsigned)rows), dim3(256), 0, s, Cm, rows, cols, pot, logw, eps, out);
+  return hipGetLastError();
+}
+
 }  // namespace amh

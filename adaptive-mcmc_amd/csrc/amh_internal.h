@@ -133,6 +133,8 @@ hipError_t run_normals(uint32_t k0, uint32_t k1, int64_t n, float* out, hipStrea
 hipError_t run_pooled_update(const PooledUpdateParams& p, hipStream_t s);
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s);
+hipError_t run_lse_rows(const float* Cm, int64_t rows, int64_t cols, const float* pot, float logw, float eps,
+                        float* out, hipStream_t s);
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
 hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);

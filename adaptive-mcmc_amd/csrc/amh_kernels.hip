@@ -20,6 +20,8 @@
 // transcendental from include/amh_math.h.  See DESIGN.md "bit spec".
 #include "amh_device.h"
 
+#include <cstdlib>
+
 namespace amh {
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -675,6 +677,508 @@ __global__ void chain_keys_kernel(uint32_t key0, uint32_t key1, int64_t offset, 
   out[2 * c + 1] = o.v[1];
 }
 
+// ------------------------------------------------------ d = 64 step kernel --
+// The headline shape (BASELINE configs[1]: the d = 64 Gaussian, one chain per
+// wave).  The same transition and the same float operations as
+// arwmh_step_kernel<64, GaussianM, true> (bit-identical, oracle: orc_step);
+// what differs is how data moves between HBM, LDS and registers:
+//
+// * Write-back through LDS.  After the DMA of item k has landed, one pass over
+//   the columns reads item k's column j from the wave's LDS buffer and, at the
+//   same addresses, writes item k-1's column j of L' = U diag(dl) (LDS is in
+//   order within a wave, so the read sees the input).  The buffer then holds
+//   item k-1's factor in the packed layout and goes to HBM as 9 full-lane
+//   buffer_store_dwordx4 instead of 64 partially masked buffer_store_dword.
+// * Exec-masked column ops.  Column j's LDS read and its normalisation touch
+//   lanes r > j only (exec set by one SALU shift inside the asm), so the unit
+//   diagonal and the zeros above it stay in the registers from the previous
+//   chain; sweep 1 runs on lanes r > j, so lane r keeps its w_r when its own
+//   column passes -- that is the forward-solve value the general kernel
+//   captures with a v_writelane per column.
+// * Broadcasts from LDS.  The per-column values every lane needs (dl_j and
+//   1/l_j in the swap, eta_j of the proposal, diff_j of the potential, and the
+//   four coefficients of sweep 2) are written once per lane into a 1 KiB
+//   per-wave scratch and read back four columns at a time with broadcast
+//   ds_read_b128, in place of v_readlane + s_nop per column.  Only sweep 1,
+//   whose w_j is serial, still uses v_readlane.
+#ifndef AMH_S64_WAVES
+#define AMH_S64_WAVES 12
+#endif
+constexpr int kS64Waves = AMH_S64_WAVES;
+typedef uint32_t uint32x4_t_ __attribute__((ext_vector_type(4)));
+constexpr int kS64P = 2080;                   // d(d+1)/2
+constexpr int kS64Z = 2080, kS64M = 2144, kS64S = 2208, kS64X = 2216;  // wave-buffer offsets (floats)
+constexpr int kS64WB = kS64X + 256;           // floats per wave buffer (9,888 B)
+constexpr int kS64Model = 64 * 68;            // GaussianM<64> rows (lds_bytes / 4)
+static_assert(kS64Z == 2080 && kS64S == kS64M + 64, "layout of prefetch_item<64>");
+constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)kS64Waves * kS64WB + 4) * sizeof(float); }
+
+constexpr int s64_col(int j) { return j * 64 - j * (j - 1) / 2; }  // packed column offset
+#ifdef AMH_S64_NOP
+#define S64_NOP "s_nop 4\n\t"
+#else
+#define S64_NOP ""
+#endif
+
+// lanes r > J read the dword at a + OFF into x (others keep x); pending until lds_wait
+template <int J, int OFF>
+__device__ __forceinline__ void s64_rd_above(float& x, uint32_t a) {
+  uint64_t sv;
+  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %3\n\t" S64_NOP "ds_read_b32 %0, %2 offset:%4\n\t" S64_NOP "s_mov_b64 exec, %1"
+               : "+v"(x), "=&s"(sv) : "v"(a), "n"(J + 1), "n"(OFF));
+}
+// lanes r >= J write v to a + OFF
+template <int J, int OFF>
+__device__ __forceinline__ void s64_wr_from(uint32_t a, float v) {
+  uint64_t sv;
+  asm volatile("s_mov_b64 %0, exec\n\ts_lshl_b64 exec, -1, %3\n\t" S64_NOP "ds_write_b32 %1, %2 offset:%4\n\t" S64_NOP "s_mov_b64 exec, %0"
+               : "=&s"(sv) : "v"(a), "v"(v), "n"(J), "n"(OFF) : "memory");
+}
+// lanes r > J: u = t * s
+template <int J>
+__device__ __forceinline__ void s64_mul_above(float& u, float t, float s) {
+  uint64_t sv;
+  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %4\n\t" S64_NOP "v_mul_f32 %0, %2, %3\n\t" S64_NOP "s_mov_b64 exec, %1"
+               : "+v"(u), "=&s"(sv) : "v"(t), "v"(s), "n"(J + 1));
+}
+// sweep 1, column J: w_J broadcast, then w -= w_J U_rJ on lanes r > J.  A VALU
+// read of an SGPR written by v_readlane needs two wait states, and SALU
+// instructions in between do not provide them (measured: with only the exec
+// setup in between, a few chains per thousand read the previous column's
+// w_j), so the s_nop 1 stays.
+template <int J>
+__device__ __forceinline__ void s64_sweep1(float& w, float u) {
+  uint64_t sv;
+  uint32_t t;
+  asm volatile("s_mov_b64 %2, exec\n\ts_lshl_b64 exec, -1, %5\n\tv_readlane_b32 %1, %0, %4\n\ts_nop 1\n\t"
+               "v_fma_f32 %0, -%1, %3, %0\n\ts_mov_b64 exec, %2"
+               : "+v"(w), "=&s"(t), "=&s"(sv) : "v"(u), "n"(J), "n"(J + 1));
+}
+__device__ __forceinline__ void s64_wr(uint32_t a, float v) {  // this lane's dword at a
+  asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
+}
+template <int OFF>
+__device__ __forceinline__ void s64_wr_off(uint32_t a, float v) {
+  asm volatile("ds_write_b32 %0, %1 offset:%2" : : "v"(a), "v"(v), "n"(OFF) : "memory");
+}
+__device__ __forceinline__ void s64_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+template <class T>
+__device__ __forceinline__ void s64_tie(T& a) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a)); }
+template <class T>
+__device__ __forceinline__ void s64_tie(T& a, T& b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)); }
+
+template <int WPB>
+__global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
+  constexpr int D = 64;
+  constexpr uint32_t P = kS64P;
+  using Gp = Grp<64>;
+  using M = GaussianM<64>;
+  extern __shared__ float lds[];
+  M::stage(lds, p.model, D);
+  float* tick = lds + kS64Model + WPB * kS64WB;
+  if (threadIdx.x == 0) tick[0] = 0.0f;
+  __syncthreads();
+  const auto mctx = M::prepare(p.model, D, lane_id());
+
+  const int64_t C = p.C;
+  const int64_t n_items = C;  // one chain per wave
+  const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb = lds + kS64Model + wave_in_block * kS64WB;
+  const uint32_t wb_a = lds_addr(wb);
+  const uint32_t x_a = wb_a + kS64X * 4;            // scratch (broadcast vectors)
+  const uint32_t prow = lds_addr(lds) + (uint32_t)lane_id() * (uint32_t)(M::ld(D) * 4);  // row r of P
+
+  float U[D];  // row r of U = L / diag(L): unit diagonal, zeros above (kept between chains)
+  static_for<D>([&](auto J) { U[J] = set_one_at<64, J>(0.0f, lane_id()); });
+  float dl = 0.0f, z = 0.0f, mu = 0.0f, pe = 0.0f, macc = 0.0f, lam = 0.0f, asc = 0.0f;
+  int32_t it = 0, nacc = 0, acc0 = 0;
+  uint32_t k0 = 0, k1 = 0;
+  int64_t prev = -1;
+  bool prev_upd = false;
+
+  const int64_t blk_lo = n_items * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t blk_hi = n_items * ((int64_t)blockIdx.x + 1) / gridDim.x;
+  const uint32_t tk_addr = lds_addr(tick);
+  auto ticket = [&]() -> int64_t {
+    uint32_t v = 0;
+    if (lane_id() == 0) {
+      asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tk_addr), "v"(1u) : "memory");
+    }
+    return blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+  };
+
+  // z, loc and the scalars of chain `c` from registers
+  auto store_small = [&](int64_t c, int r) {
+    p.out.z[c * D + r] = z;
+    p.out.loc[c * D + r] = mu;
+    if (r == 0) {
+      p.out.i[c] = it;
+      p.out.potential_energy[c] = pe;
+      p.out.mean_accept_prob[c] = macc;
+      p.out.log_step_size[c] = lam;
+      p.out.as_change[c] = asc;
+      p.out.rng_key[2 * c] = k0;
+      p.out.rng_key[2 * c + 1] = k1;
+      if (p.accept_count != nullptr) p.accept_count[c] = acc0 + nacc;
+    }
+  };
+  // factor of chain `c` copied verbatim from the launch input (no step of this
+  // launch updated it); U is used as scratch and reset to the unit pattern
+  auto copy_verbatim = [&](int64_t c, int r) {
+    const uint32_t vrow = (uint32_t)r * 4u;
+    const Buf Lout(uniform_ptr(p.out.scale + c * P), P * 4u);
+    const Buf Lin(uniform_ptr(p.in.scale + c * P), P * 4u);
+    static_for<4>([&](auto B) {
+      static_for<16>([&](auto K) {
+        constexpr int j = 16 * B + K;
+        U[j] = Lin.ld(off_from<64, j>(vrow, kOOB, r), (uint32_t)(s64_col(j) - j) * 4u);
+      });
+      static_for<16>([&](auto K) {
+        constexpr int j = 16 * B + K;
+        Lout.st(U[j], off_from<64, j>(vrow, kOOB, r), (uint32_t)(s64_col(j) - j) * 4u);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_s_waitcnt(0);  // loads landed and store data read before U is reused
+    static_for<D>([&](auto J) { U[J] = set_one_at<64, J>(0.0f, r); });
+  };
+  // the wave buffer's factor region (packed, column-major) -> chain `c` in HBM
+  auto flush_factor = [&](int64_t c) {
+    const Buf Lout(uniform_ptr(p.out.scale + c * P), P * 4u);
+    const uint32_t la = wb_a + (uint32_t)lane_id() * 16u;
+    f32x4 v[9];
+    v[0] = lds_ld4<0>(la); v[1] = lds_ld4<1024>(la); v[2] = lds_ld4<2048>(la);
+    v[3] = lds_ld4<3072>(la); v[4] = lds_ld4<4096>(la); v[5] = lds_ld4<5120>(la);
+    v[6] = lds_ld4<6144>(la); v[7] = lds_ld4<7168>(la); v[8] = lds_ld4<8192>(la);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
+                 "+v"(v[6]), "+v"(v[7]), "+v"(v[8]));
+    static_for<9>([&](auto Q) {
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32x4_t_, v[(int)Q]), Lout.rs,
+                                             (int)(1024u * Q + 16u * (uint32_t)lane_id()), 0, AMH_STORE_AUX);
+    });
+  };
+
+  int64_t item = ticket();
+  int64_t nxt = item < blk_hi ? ticket() : blk_hi;
+  if (item < blk_hi) prefetch_item<64, false>(p, item, D, wb, lane_id());
+  for (; item < blk_hi;) {
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const int r = lane;
+    const uint32_t la = wb_a + (uint32_t)r * 4u;  // this lane's dword in the factor region
+
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): item k has landed
+    // ---- item k-1's z / loc / scalars leave from registers
+    if (prev >= 0) store_small(prev, r);
+    const bool wr = prev >= 0 && prev_upd;
+    if (prev >= 0 && !prev_upd) copy_verbatim(prev, r);
+
+    // ---- diagonal of item k; broadcast vectors [dl of k-1 | 1 / l of k]
+    float lnew = lds_ld1<0>(wb_a + (uint32_t)s64_col(r) * 4u);
+    s64_tie(lnew);
+    const float inv = (amh_isfinite(lnew) && lnew != 0.0f) ? 1.0f / lnew : 0.0f;
+    s64_wr(x_a + (uint32_t)r * 4u, dl);
+    s64_wr_off<256>(x_a + (uint32_t)r * 4u, inv);
+
+    // ---- swap: read item k's column j (lanes > j), write item k-1's column j
+    //      of L' = U diag(dl) (lanes >= j) at the same addresses, normalise
+    static_for<16>([&](auto G4) {
+      constexpr int g = G4;
+      f32x4 dl4 = lds_ld4<16 * g>(x_a);
+      f32x4 in4 = lds_ld4<256 + 16 * g>(x_a);
+      s64_tie(dl4, in4);
+      float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      static_for<4>([&](auto Q) {
+        constexpr int j = 4 * g + Q;
+        constexpr int off = (s64_col(j) - j) * 4;
+        if constexpr (j < D - 1) s64_rd_above<j, off>(t[(int)Q], la);
+        if (wr) s64_wr_from<j, off>(la, U[j] * dl4[(int)Q]);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]));
+      static_for<4>([&](auto Q) {
+        constexpr int j = 4 * g + Q;
+        if constexpr (j < D - 1) s64_mul_above<j>(U[j], t[(int)Q], in4[(int)Q]);
+      });
+    });
+    if (wr) flush_factor(prev);
+
+    // ---- item k's z / loc / scalars: LDS -> registers
+    {
+      float zz = lds_ld1<kS64Z * 4>(la), mm = lds_ld1<kS64M * 4>(la);
+      const uint32_t sa = wb_a + kS64S * 4;
+      float s0 = lds_ld1<0>(sa), s1 = lds_ld1<4>(sa), s2 = lds_ld1<8>(sa), s3 = lds_ld1<12>(sa);
+      float s4v = lds_ld1<16>(sa), s5 = lds_ld1<20>(sa), s6 = lds_ld1<24>(sa);
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(zz), "+v"(mm), "+v"(s0), "+v"(s1), "+v"(s2), "+v"(s3), "+v"(s4v),
+                   "+v"(s5), "+v"(s6));
+      z = zz;
+      mu = mm;
+      it = __builtin_amdgcn_readfirstlane(__float_as_int(s0));
+      pe = s1;
+      macc = s2;
+      lam = s3;
+      asc = s4v;
+      k0 = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s5));
+      k1 = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s6));
+      dl = lnew;
+      acc0 = (p.accept_count != nullptr && r == 0) ? p.accept_count[item] : 0;
+    }
+    s64_wait();  // every LDS read of the buffer is done before the DMA refills it
+    int64_t nxt2 = blk_hi;
+    if (nxt < blk_hi) {
+      prefetch_item<64, false>(p, nxt, D, wb, lane);
+      nxt2 = ticket();
+    }
+
+    nacc = 0;
+    bool updated = false;
+    for (int32_t t = 0; t < p.n_steps; ++t) {
+      // ---- noise (arwmh.py:162-165, 174): stream position = state.i
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+      const float xi = amh_normal_from_bits(o.v[0]);
+      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+
+      // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167), L xi = U (dl * xi)
+      const float el = amh_expf(lam);
+      const float eta = dl * xi;
+#ifndef AMH_S64_BC_RL
+      s64_wr(x_a + (uint32_t)r * 4u, eta);
+#endif
+      float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      static_for<4>([&](auto B) {  // 16 columns per batch
+        constexpr int b = B;
+        f32x4 e[4];
+#ifndef AMH_S64_BC_RL
+        e[0] = lds_ld4<64 * b>(x_a);
+        e[1] = lds_ld4<64 * b + 16>(x_a);
+        e[2] = lds_ld4<64 * b + 32>(x_a);
+        e[3] = lds_ld4<64 * b + 48>(x_a);
+        lds_wait(e[0], e[1], e[2], e[3]);
+#else
+        static_for<16>([&](auto K) { e[(int)K / 4][(int)K % 4] = Gp::template bcast<16 * b + K>(eta); });
+#endif
+        static_for<16>([&](auto K) {
+          constexpr int j = 16 * b + K;
+          a4[j & 3] = fmaf(U[j], e[(int)K / 4][(int)K % 4], a4[j & 3]);
+        });
+        __builtin_amdgcn_sched_barrier(0);
+      });
+      const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+      const float zp = z + fmaf(el, acc, p.eps * xi);
+
+      // ---- potential (GaussianM<64>::potential with diff_j from the scratch), NaN -> +inf
+      float pep;
+      {
+        const float diff = zp - mctx.mr;
+#ifndef AMH_S64_BC_RL
+        s64_wr(x_a + (uint32_t)r * 4u, diff);
+#endif
+        f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
+        static_for<4>([&](auto B) {
+          constexpr int b = B;
+          f32x4 pv[4], dv[4];
+          static_for<4>([&](auto Q) {
+            pv[(int)Q] = lds_ld4<16 * (4 * b + Q)>(prow);
+#ifndef AMH_S64_BC_RL
+            dv[(int)Q] = lds_ld4<16 * (4 * b + Q)>(x_a);
+#else
+            static_for<4>([&](auto K) { dv[(int)Q][(int)K] = Gp::template bcast<16 * b + 4 * Q + K>(diff); });
+#endif
+          });
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
+                       "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+          static_for<8>([&](auto K2) {
+            const f32x4 q = pv[(int)K2 / 2];
+            const f32x4 dq = dv[(int)K2 / 2];
+            const f32x2v pp = (K2 % 2 == 0) ? f32x2v{q[0], q[1]} : f32x2v{q[2], q[3]};
+            const f32x2v bp = (K2 % 2 == 0) ? f32x2v{dq[0], dq[1]} : f32x2v{dq[2], dq[3]};
+            if constexpr (K2 % 2 == 0) {
+              y01 = __builtin_elementwise_fma(pp, bp, y01);
+            } else {
+              y23 = __builtin_elementwise_fma(pp, bp, y23);
+            }
+          });
+          __builtin_amdgcn_sched_barrier(0);
+        });
+        const float y = (y01[0] + y01[1]) + (y23[0] + y23[1]);
+        const float S = Gp::sum(diff * y);
+        pep = (0.5f * S) + mctx.c0;
+      }
+      if (amh_isnan(pep)) pep = INFINITY;
+
+      // ---- accept / reject (arwmh.py:173-178)
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      const bool accept = u < alpha;
+      const float zn = accept ? zp : z;
+      const float pen = accept ? pep : pe;
+      nacc += accept ? 1 : 0;
+
+      // ---- schedule (arwmh.py:180-185)
+      const int32_t itr = it + 1;
+      const int32_t n = (it < p.W) ? itr : itr - p.W;
+      const float gamma = lookup_gamma<64>(p, n);
+      const float maccn = macc + (alpha - macc) / (float)n;
+
+      // ---- mean and step size (arwmh.py:188-189, 193)
+      const float delta = zn - mu;
+      const float mun = mu + gamma * delta;
+      const float lamn = lam + gamma * (alpha - p.target);
+      const float e1 = amh_expf(lamn);
+
+      // ---- rank-one update of sqrt(1-gamma) L by (delta, gamma), NaN -> keep L
+      const float sq = sqrtf(1.0f - gamma);
+      const float ajj = sq * dl;
+      const float Dg = ajj * ajj;
+      const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+
+      // sweep 1 (lanes r > j): afterwards lane r holds w*_r (forward solve U w* = delta)
+#ifndef AMH_S64_SW1_OLD
+      float ws = delta;
+      static_for<D - 1>([&](auto J) {
+        s64_sweep1<J>(ws, U[J]);
+        column_fence<J>();
+      });
+#else
+      float ws = 0.0f;
+      {
+        float w = delta;
+        static_for<D>([&](auto J) {
+          const float wj = Gp::template bcast<J>(w);
+          ws = capture<64, J>(ws, wj, r);
+          w = fmaf(-wj, U[J], w);
+          column_fence<J>();
+        });
+      }
+#endif
+
+      const float gw2 = gamma * (ws * ws);
+      const float tsc = gw2 / Dg;
+      const float b = 1.0f + Gp::excl_scan(tsc, r);
+      const float g2 = (b * Dg) + gw2;
+      const float dn = g2 / b;
+      const float c = (gamma * ws) / g2;
+      const float q = sqrtf(dn);
+      const float dnew = fmaf(c, 0.0f, one) * q;
+      const bool revert = Gp::any(amh_isnan(dnew));
+      float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (!revert) {
+        // sweep 2: U'_rj = U_rj + c_j w_r^{(j+1)}; as_change terms
+        //   U_rj (q_j e1 - dl_j e0) + (c_j q_j e1) w_r^{(j+1)}
+        const float ac = (q * e1) - (dl * el);
+        const float bc = (c * q) * e1;
+#ifndef AMH_S64_BC_RL
+        s64_wr(x_a + (uint32_t)r * 4u, ws);
+        s64_wr_off<256>(x_a + (uint32_t)r * 4u, c);
+        s64_wr_off<512>(x_a + (uint32_t)r * 4u, ac);
+        s64_wr_off<768>(x_a + (uint32_t)r * 4u, bc);
+#endif
+        float w = delta;
+        static_for<16>([&](auto G4) {
+          constexpr int g = G4;
+#ifndef AMH_S64_BC_RL
+          f32x4 cw = lds_ld4<16 * g>(x_a), cc = lds_ld4<256 + 16 * g>(x_a);
+          f32x4 ca = lds_ld4<512 + 16 * g>(x_a), cb = lds_ld4<768 + 16 * g>(x_a);
+          lds_wait(cw, cc, ca, cb);
+#else
+          f32x4 cw, cc, ca, cb;
+          static_for<4>([&](auto Q) {
+            cw[(int)Q] = Gp::template bcast<4 * g + Q>(ws);
+            cc[(int)Q] = Gp::template bcast<4 * g + Q>(c);
+            ca[(int)Q] = Gp::template bcast<4 * g + Q>(ac);
+            cb[(int)Q] = Gp::template bcast<4 * g + Q>(bc);
+          });
+#endif
+          static_for<4>([&](auto Q) {
+            constexpr int j = 4 * g + Q;
+            const float uo = U[j];
+            w = fmaf(-cw[(int)Q], uo, w);
+            const float un = fmaf(cc[(int)Q], w, uo);
+            const float tt = fmaf(uo, ca[(int)Q], cb[(int)Q] * w);
+            s4[j & 3] = fmaf(tt, tt, s4[j & 3]);
+            U[j] = un;
+          });
+          column_fence<g, 2>();
+        });
+        const float sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        asc = sqrtf(Gp::sum(sacc));
+        dl = q;
+        updated = true;
+      } else {
+        // factor unchanged: as_change = || L (e1 - e0) ||_F, L_rj = U_rj dl_j
+        const float ac = (dl * e1) - (dl * el);
+        static_for<D>([&](auto J) {
+          const float tt = U[J] * Gp::template bcast<J>(ac);
+          s4[J & 3] = fmaf(tt, tt, s4[J & 3]);
+          column_fence<J>();
+        });
+        const float sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+        asc = sqrtf(Gp::sum(sacc));
+      }
+
+      // ---- commit (arwmh.py:199-207)
+      it = itr;
+      z = zn;
+      pe = pen;
+      macc = maccn;
+      mu = mun;
+      lam = lamn;
+      if (p.col_z != nullptr || p.col_pe != nullptr) {
+        if ((t + 1) % p.thinning == 0) {
+          const int64_t kk = t / p.thinning;
+          if (p.col_z != nullptr) p.col_z[(kk * C + item) * D + r] = z;
+          if (p.col_pe != nullptr && r == 0) p.col_pe[kk * C + item] = pe;
+        }
+      }
+    }
+    prev = item;
+    prev_upd = Gp::any(updated);
+    item = nxt;
+    nxt = nxt2;
+  }
+  if (prev >= 0) {
+    int lane = lane_id();
+    asm volatile("" : "+v"(lane));
+    const uint32_t la = wb_a + (uint32_t)lane * 4u;
+    store_small(prev, lane);
+    if (prev_upd) {
+      s64_wr(x_a + (uint32_t)lane * 4u, dl);
+      static_for<16>([&](auto G4) {
+        constexpr int g = G4;
+        f32x4 dl4 = lds_ld4<16 * g>(x_a);
+        s64_tie(dl4);
+        static_for<4>([&](auto Q) {
+          constexpr int j = 4 * g + Q;
+          s64_wr_from<j, (s64_col(j) - j) * 4>(la, U[j] * dl4[(int)Q]);
+        });
+      });
+      flush_factor(prev);
+    } else {
+      copy_verbatim(prev, lane);
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0);
+}
+
+template <int WPB>
+hipError_t launch_step64(const StepParams& p, hipStream_t s) {
+  constexpr size_t shm = s64_lds_bytes();
+  static_assert(shm <= 163840, "d = 64 step kernel: LDS budget");
+  auto kern = arwmh_step64_kernel<WPB>;
+  int per_cu = 0;
+  hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, shm);
+  if (e != hipSuccess) return e;
+  int dev = 0, cus = 0;
+  (void)hipGetDevice(&dev);
+  (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (per_cu < 1) per_cu = 1;
+  const int64_t need = (p.C + WPB - 1) / WPB;
+  int64_t blocks = (int64_t)cus * per_cu;
+  if (blocks > need) blocks = need;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(WPB * 64), shm, s, p);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------- launchers ----
 static int grid_for(int64_t n_items, int waves_per_block) {
   // enough waves to cover 256 CUs x 8 waves/CU several times; grid-stride past it
@@ -761,7 +1265,28 @@ struct PnxF {
   hipError_t operator()() { return launch_pnx<D, M, E>(p, s); }
 };
 
+static bool step64_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("AMH_STEP64");
+    return !(e != nullptr && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
+  // the headline shape: d = 64 Gaussian, LDS-staged write-back (AMH_STEP64=0 selects the general kernel)
+  if (model_id == AMH_MODEL_GAUSSIAN && p.d == 64 && p.ext_pe == nullptr && step64_enabled()) {
+    static const bool move_only = [] {  // diagnostic: the data movement alone (tools/membound.py)
+      const char* e = getenv("AMH_S64_MOVE_ONLY");
+      return e != nullptr && e[0] == '1';
+    }();
+    if (move_only) {
+      StepParams q = p;
+      q.n_steps = 0;
+      return launch_step64<kS64Waves>(q, s);
+    }
+    return launch_step64<kS64Waves>(p, s);
+  }
   // diamonds at the reference shape: compile-time d (immediate offsets)
   if (model_id == AMH_MODEL_DIAMONDS_SS && p.d == kDiamondsD) return launch_step<32, DiamondsSSM, false, kDiamondsD>(p, s);
   return dispatch(model_id, p.d, StepF{p, s});

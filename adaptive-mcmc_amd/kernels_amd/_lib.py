@@ -30,7 +30,7 @@ EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bi
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
-           "amh_normals")
+           "amh_normals", "amh_sinkhorn_lse")
 
 
 class AmhConfig(ctypes.Structure):
@@ -98,6 +98,8 @@ def lib():
     L.amh_pairwise_dist2.restype = ctypes.c_int
     L.amh_normals.argtypes = [ctypes.POINTER(ctypes.c_uint32), I64, P, P]
     L.amh_normals.restype = ctypes.c_int
+    L.amh_sinkhorn_lse.argtypes = [P, I64, I64, P, F, F, P, P]
+    L.amh_sinkhorn_lse.restype = ctypes.c_int
     for name in EXPORTS[:10]:
         getattr(L, name).restype = ctypes.c_int if name != "amh_last_error" else ctypes.c_char_p
     _lib = L

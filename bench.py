@@ -176,6 +176,30 @@ def timed_region(ctx, fn):
 
 
 # ------------------------------------------------------------------- legs --
+CLOCK_WARM_S = 0.3
+
+
+def clock_warm(step, ctx, seconds: float = CLOCK_WARM_S):
+    """Untimed launches for a fixed wall time before the timed region.  After
+    an idle gap the GPU needs ~30 ms (~100 launches) of back-to-back step
+    launches to reach its steady clocks (tools/ramp.py: 0.30-0.34 ms per
+    launch at first, 0.258 ms after), so a 5-step warmup times
+    the ramp, not the kernel.  These are real transitions: the chains just
+    advance further before the timed steps.  Reported as `clock_warm`."""
+    import torch
+    t0 = time.perf_counter()
+    n = 0
+    while True:  # every rank takes the same decision (pooled legs run collectives per step)
+        for _ in range(25):
+            step()
+        n += 25
+        torch.cuda.synchronize()
+        if ctx.max_over_ranks(time.perf_counter() - t0) >= seconds:
+            break
+    ctx.barrier()
+    return {"seconds": round(time.perf_counter() - t0, 3), "launches": n}
+
+
 def leg_regime_a(ctx, g, C, off, steps, warmup):
     """ARWMH.sample per step (per-chain adaptation); HIP events on the launch
     stream bracket the step launches only."""
@@ -189,6 +213,7 @@ def leg_regime_a(ctx, g, C, off, steps, warmup):
     st = k.init(PRNGKey(0), 0, z0, (), {})
     for _ in range(warmup):
         k.sample_(st, 1)
+    warm = clock_warm(lambda: k.sample_(st, 1), ctx)
     stream = torch.cuda.current_stream(ctx.dev)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
@@ -200,7 +225,7 @@ def leg_regime_a(ctx, g, C, off, steps, warmup):
 
     wall = timed_region(ctx, run)
     kern_ms = ev0.elapsed_time(ev1) / steps
-    return dict(wall=wall, kern_ms=kern_ms, kernel=k, state=st)
+    return dict(wall=wall, kern_ms=kern_ms, kernel=k, state=st, clock_warm=warm)
 
 
 def leg_pooled(ctx, g, C, off, steps, warmup, K=1, overlap=False, burn_in=0):
@@ -217,8 +242,9 @@ def leg_pooled(ctx, g, C, off, steps, warmup, K=1, overlap=False, burn_in=0):
     z0 = (torch.rand(C, g.dim, device=ctx.dev, generator=gen) * 4.0 - 2.0).contiguous()
     st = k.init(PRNGKey(0), 0, z0, (), {})
     k.sample_(st, burn_in + warmup)
+    warm = clock_warm(lambda: k.sample_(st, K), ctx)
     wall = timed_region(ctx, lambda: k.sample_(st, steps))
-    return dict(wall=wall, steps=steps, kernel=k, state=st, burn_in=burn_in, warmup=warmup)
+    return dict(wall=wall, steps=steps, kernel=k, state=st, burn_in=burn_in, warmup=warmup, clock_warm=warm)
 
 
 def pooled_stats_ms(k, st, C, reps=20):
@@ -256,7 +282,7 @@ def pooled_line(ctx, r, total, d, C):
             "ms_per_step": r["wall"] / r["steps"] * 1e3, "steps": r["steps"], "chains_per_gpu": C,
             "chains_total": total, "sync_every": K, "overlap": bool(k.overlap), "burn_in": r["burn_in"],
             "mean_accept_prob": float(st.mean_accept_prob[0]), "allreduce_doubles": d + d * (d + 1) // 2 + 2,
-            "collective": coll}
+            "collective": coll, "clock_warm": r["clock_warm"]}
 
 
 def ess_leg(ctx, g, burn_in=20000, T=1000, Cs=4096):
@@ -376,7 +402,8 @@ def main():
                 "config": {"workload": (f"ARWMH.sample, d={d} correlated Gaussian, {C} chains, per-chain "
                                         f"adaptation (BASELINE.json configs[1])"),
                            "chains_per_gpu": C, "dim": d, "parallelism": "1 GPU"},
-                "roofline": roofline, "cpu_baseline": cpu, "ess": ess, "fused_chain_steps_per_s": fused, **sub}
+                "roofline": roofline, "cpu_baseline": cpu, "clock_warm": r["clock_warm"], "ess": ess,
+                "fused_chain_steps_per_s": fused, **sub}
         print(json.dumps(line), flush=True)
         return
 
@@ -404,7 +431,7 @@ def main():
                 pr = leg_pooled(ctx, g, C, rank * C, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
                 sub[name] = pooled_line(ctx, pr, total, d, C)
         ra = leg_regime_a(ctx, g, C, rank * C, args.steps, args.warmup)
-        sub["regime_a"] = {"value": total * args.steps / ra["wall"], "unit": "chain-steps/s",
+        sub["regime_a"] = {"value": total * args.steps / ra["wall"], "unit": "chain-steps/s", "clock_warm": ra["clock_warm"],
                            "ms_per_step": ra["wall"] / args.steps * 1e3, "kernel_ms": ra["kern_ms"],
                            "collective": "none (chains independent, BASELINE configs[1] per GPU)"}
     if rank == 0:
@@ -415,7 +442,7 @@ def main():
                                         f"({total} in total), all_reduce(sum) of the pooled sums every step "
                                         f"(BASELINE.json configs[4])"),
                            "chains_per_gpu": C, "dim": d, "parallelism": ctx.parallelism(f"chains sharded x{world}")},
-                "roofline": roofline, "cpu_baseline": None, "pooled": head, **sub}
+                "roofline": roofline, "cpu_baseline": None, "clock_warm": head["clock_warm"], "pooled": head, **sub}
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 

@@ -176,6 +176,13 @@ int amh_kernel_sum(const float* a, int64_t n, const float* b, int64_t m, int32_t
                    int32_t skip_diag, double* scratch, double* out, void* stream);
 /* out[i] = standard normal i of the stream keyed by key[2] (host memory),
  * for the random directions of max_sliced_wasserstein (evaluation.py:189). */
+/* One half-iteration of log-domain Sinkhorn (the OT solver behind
+ * wasserstein_sinkhorn, python/utils/evaluation.py:69-101, ott-jax linear.solve):
+ * out[i] = -eps * log sum_j exp((pot[j] - cost[i][j]) / eps + log_w), cost
+ * row-major [rows][cols] on the device.  The other half runs on the
+ * transposed cost matrix. */
+int amh_sinkhorn_lse(const float* cost, int64_t rows, int64_t cols, const float* pot, float log_w, float eps,
+                     float* out, void* stream);
 int amh_normals(const uint32_t key[2], int64_t n, float* out, void* stream);
 /* out [n][m] = ||a_i - b_j||^2 (the median bandwidth heuristic, evaluation.py:286). */
 int amh_pairwise_dist2(const float* a, int64_t n, const float* b, int64_t m, int32_t d, float* out,

@@ -23,5 +23,7 @@ def test_world_mismatch_refused():
 
 def test_self_spawn_starts_n_ranks():
     r = _run(["--gpus", "2", "--steps", "1", "--warmup", "0", "--no-extra"], {})
-    assert r.returncode != 0  # no GPU in this container: every rank stops at the device check
-    assert (r.stderr + r.stdout).count("no GPU visible") == 2
+    assert r.returncode != 0  # no GPU in this container: the ranks stop at the device check
+    # (the parent stops the other rank once one has failed, so it may not get to print)
+    assert 1 <= (r.stderr + r.stdout).count("no GPU visible") <= 2
+    assert "WORLD_SIZE" not in (r.stderr + r.stdout)  # the children got the launcher environment

@@ -91,3 +91,47 @@ def test_mmd_of_asss_draws_vs_reference_sample(gpu):
     same = E.mmd2_unbiased(a, b, 0.25)
     shifted = E.mmd2_unbiased(a, b + 0.5, 0.25)
     assert abs(same) < 0.003 and shifted > 10 * abs(same)
+
+
+@pytest.mark.parametrize("n,m,d,cost_fn", [(300, 257, 26, "euclidean"), (128, 500, 3, "sqeuclidean"),
+                                           (1000, 1000, 10, "euclidean")])
+def test_sinkhorn_against_float64(n, m, d, cost_fn, gpu):
+    """wasserstein_sinkhorn (evaluation.py:69-101) on the HIP log-sum-exp
+    half-iterations vs the float64 restatement (oracle/sinkhorn_np.py), same
+    iteration order: potentials after a fixed 40 iterations within 1e-4 eps,
+    the converged cost within 1e-4 relative.  Parity against ott-jax itself is
+    unpinned (not importable)."""
+    import sinkhorn_np as S
+    from utils_amd import evaluation as E
+    rng = np.random.default_rng(n + d)
+    x = rng.normal(size=(n, d)).astype(np.float32)
+    y = (rng.normal(size=(m, d)) * 0.8 + 0.5).astype(np.float32)
+    got = E.sinkhorn(x, y, cost_fn=cost_fn, threshold=0.0, max_iterations=40)
+    ref = S.sinkhorn(x, y, cost_fn=cost_fn, threshold=0.0, max_iterations=40)
+    assert got["epsilon"] == pytest.approx(ref["epsilon"], rel=1e-5)
+    eps = ref["epsilon"]
+    np.testing.assert_allclose(got["f"].cpu().numpy(), ref["f"], rtol=0, atol=1e-4 * max(eps, 1.0))
+    np.testing.assert_allclose(got["g"].cpu().numpy(), ref["g"], rtol=0, atol=1e-4 * max(eps, 1.0))
+    a = E.sinkhorn(x, y, cost_fn=cost_fn)
+    b = S.sinkhorn(x, y, cost_fn=cost_fn)
+    assert a["converged"] and b["converged"] and a["error"] < 1e-3
+    assert a["cost"] == pytest.approx(b["cost"], rel=1e-4)
+    assert E.wasserstein_sinkhorn(x, y, cost_fn=cost_fn) == pytest.approx(b["cost"], rel=1e-4)
+
+
+def test_sinkhorn_unbiased_and_exact_limit(gpu):
+    """The unbiased divergence of a set with itself is 0, it is symmetric, and
+    with a small epsilon the regularised cost approaches the exact optimal
+    1-1 coupling cost (scipy's Hungarian, wasserstein_dist11_p)."""
+    from utils_amd import evaluation as E
+    rng = np.random.default_rng(11)
+    x = rng.normal(size=(200, 4)).astype(np.float32)
+    y = (rng.normal(size=(200, 4)) + 0.7).astype(np.float32)
+    assert abs(E.wasserstein_sinkhorn_unbiased(x, x)) < 1e-5
+    uv, vu = E.wasserstein_sinkhorn_unbiased(x, y), E.wasserstein_sinkhorn_unbiased(y, x)
+    assert uv == pytest.approx(vu, rel=1e-4) and uv > 0
+    exact = E.wasserstein_dist11_p(x, y, ord=2.0)
+    r = E.sinkhorn(x, y, epsilon=0.01, threshold=1e-4, max_iterations=20000)
+    assert r["converged"]
+    # dual cost = <P, C> + eps KL(P | a b^T) with 0 <= KL <= log n
+    assert exact - 1e-4 <= r["cost"] <= exact + 0.01 * np.log(200) + 1e-4
