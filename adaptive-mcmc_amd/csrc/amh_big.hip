@@ -543,6 +543,11 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
 
 // ------------------------------------------------------------- launchers ----
 bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256 && d % 32 == 0; }
+// pooled mode: the MFMA path also takes d = 64 (every per-chain product is a
+// GEMM over chains once the factor is shared)
+bool pooled_big_model(int model_id, int d) {
+  return model_id == AMH_MODEL_GAUSSIAN && d >= 64 && d <= 256 && d % 32 == 0;
+}
 
 static int wave_grid(int64_t n) {
   int64_t b = (n + 3) / 4;

@@ -1,6 +1,7 @@
-// amh_big_pooled.hip -- pooled-covariance mode (regime B) for 64 < d <= 256
-// (Gaussian, d % 32 == 0): BASELINE config 4's headline, d = 256 with one
-// shared factor for 32,768 chains.
+// amh_big_pooled.hip -- pooled-covariance mode (regime B) for the Gaussian
+// with d % 32 == 0, 64 <= d <= 256: BASELINE config 4's headline (d = 256,
+// one shared factor for 32,768 chains) and config 5's per-GPU work (d = 64,
+// 65,536 chains, pooled_fused64_kernel).
 //
 // With one shared L every per-chain product is a GEMM over chains, so the
 // three O(d^2) pieces run on MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf
@@ -247,6 +248,209 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
       });
     }
   });
+}
+
+// -------------------------------------------------- fused stats, d = 64 --
+// BASELINE configs[4]'s per-GPU work (d = 64, 65,536 chains): the three
+// launches above in one, one 64-chain chunk per 256-thread block (the chunk
+// size of the d = 64 bit spec; 1,024 blocks at the config, two resident per
+// CU), with the shared factor L and the precision P staged in LDS instead of
+// read from L2 per MFMA; the blocks are persistent (two per CU) and walk the
+// chunks, so P and L are staged once per block.  Steps: z and xi -> LDS; proposal on MFMA (wave w:
+// row tile w >> 1, chain half w & 1); xprop = z + fmaf(e^lam, L xi, eps xi);
+// U(xprop) on MFMA with D = xprop - m formed as the B operand is read;
+// accept; delta = z' - mu in place of z; S_d, S_a sequential and S_dd on MFMA
+// (waves 0..2: tile pairs (0,0), (1,0), (1,1)).  Every float operation and
+// its order are those of pooled_big_propose_kernel + gauss_pot_mfma_kernel +
+// pooled_big_stats_kernel (oracle: orc_pooled_stats_big).
+constexpr int kF = 64;      // d
+constexpr int kFLd = 65;    // LDS row stride
+constexpr int kFChunk = 64; // chains per chunk at d = 64 (bit spec)
+constexpr size_t fused64_lds_bytes() { return ((size_t)4 * kF * kFLd + 2 * 64 + 4 * 64) * sizeof(float); }
+
+__global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParams p, int64_t n_chunks) {
+  extern __shared__ float lds[];
+  constexpr int d = kF;
+  constexpr int64_t P = d * (d + 1) / 2;
+  constexpr int64_t V = d + P + 2;
+  float* Pm = lds;                       // [r][k] precision rows
+  float* Lm = Pm + d * kFLd;             // [r][k] shared factor rows (0 above the diagonal)
+  float* Zb = Lm + d * kFLd;             // [k][chain] z, then delta
+  float* Xb = Zb + d * kFLd;             // [k][chain] xi, then xprop
+  float* tsum = Xb + d * kFLd;           // [2][64]
+  float* uu = tsum + 2 * 64;             // [64] uniform of the accept test
+  int* flag = (int*)(uu + 64);           // [64]
+  float* alph = (float*)(flag + 64);     // [64]
+  float* msh = alph + 64;                // [64] target mean m
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
+  const int h = lane >> 5, i = lane & 31;
+  const float c0p = p.model.data[d + d * d];
+  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
+  const float el = amh_expf(p.lam[0]);
+  const float mu_l = p.mu[lane];  // lane = coordinate k in the chain-major phases
+  const int T = w >> 1, hf = w & 1;  // proposal / potential: row tile, chain half
+  // P and L staged once per (persistent) block: 16 loads per thread in flight
+  {
+    float pv[16], lv[16];
+    static_for<16>([&](auto N) {
+      const int idx = tid + 256 * N;
+      const int r = idx / d, k = idx - r * d;
+      pv[N] = p.model.data[d + idx];
+      lv[N] = (k <= r) ? p.L[pk(d, r, k)] : 0.0f;
+    });
+    static_for<16>([&](auto N) {
+      const int idx = tid + 256 * N;
+      const int r = idx / d, k = idx - r * d;
+      Pm[r * kFLd + k] = pv[N];
+      Lm[r * kFLd + k] = lv[N];
+    });
+    if (tid < d) msh[tid] = p.model.data[tid];
+  }
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+  const int64_t c0 = chunk * kFChunk;
+  const int64_t left = p.C - c0;
+  const int nv = left < kFChunk ? (int)left : kFChunk;
+  // (1) z and the noise xi (arwmh.py:162-165), k-major; wave w takes the
+  // chains w, w + 4, ..; lane = coordinate k.  All loads are issued first.
+  float pe_c = 0.0f;
+  {
+    float zv[16];
+    uint32_t k0v[16], k1v[16];
+    static_for<16>([&](auto N) {
+      int64_t ch = c0 + w + 4 * N;
+      if (ch >= p.C) ch = p.C - 1;
+      zv[N] = p.z[ch * d + lane];
+      k0v[N] = p.keys[2 * ch];
+      k1v[N] = p.keys[2 * ch + 1];
+    });
+    pe_c = (tid < nv) ? p.pe[c0 + tid] : 0.0f;
+    __syncthreads();  // the previous chunk's readers of Zb / Xb / uu are done
+    static_for<16>([&](auto N) {
+      const int cc = w + 4 * N;
+      Zb[lane * kFLd + cc] = zv[N];
+#ifndef AMH_F64_NORNG
+      const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)it, 0u, AMH_TAG_STEP, k0v[N], k1v[N]);
+      Xb[lane * kFLd + cc] = amh_normal_from_bits(o.v[0]);
+      if (lane == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
+#else
+      Xb[lane * kFLd + cc] = (float)((k0v[N] + lane) & 15) * 0.1f - 0.75f;
+      if (lane == 0) uu[cc] = 0.5f;
+#endif
+    });
+  }
+  __syncthreads();
+  // (2) proposal: acc = L xi over k < 32 (T + 1) (arwmh.py:166-167)
+  {
+    f32x16 acc = f32x16{};
+    const int kend = 32 * (T + 1);
+    const int arow = (32 * T + i) * kFLd + h;
+#ifndef AMH_F64_NOPROP
+    for (int kk = 0; kk < kend; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Lm[arow + kk], Xb[(kk + h) * kFLd + 32 * hf + i], acc, 0, 0, 0);
+#endif
+    float v[16];
+    static_for<16>([&](auto R) {
+      const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+      v[R] = fmaf(el, acc[(int)R], p.eps * Xb[rr * kFLd + 32 * hf + i]);
+    });
+    __syncthreads();
+    static_for<16>([&](auto R) {
+      const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+      const int o = rr * kFLd + 32 * hf + i;
+      Xb[o] = Zb[o] + v[R];  // xprop = z + (e^lam L xi + eps xi)
+    });
+  }
+  __syncthreads();
+  // (3) U(xprop) on MFMA: Y = P D with D = xprop - m, q_r = D_r y_r
+  {
+    f32x16 acc = f32x16{};
+    const int arow = (32 * T + i) * kFLd + h;
+#ifndef AMH_F64_NOPOT
+    for (int kk = 0; kk < d; kk += 2)
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Pm[arow + kk], Xb[(kk + h) * kFLd + 32 * hf + i] - msh[kk + h], acc,
+                                                 0, 0, 0);
+#endif
+    float ps = 0.0f;
+    static_for<16>([&](auto R) {
+      const int row = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+      ps = ps + (Xb[row * kFLd + 32 * hf + i] - msh[row]) * acc[(int)R];
+    });
+    const float other = __shfl_xor(ps, 32, 64);
+    const float tI = (h == 0) ? ps + other : other + ps;
+    if (h == 0) tsum[T * 64 + 32 * hf + i] = tI;
+  }
+  __syncthreads();
+  // (4) accept / reject (arwmh.py:173-178)
+  if (tid < 64) {
+    int acc_f = 0;
+    float a = 0.0f;
+    if (tid < nv) {
+      float S = 0.0f;
+      S = S + tsum[tid];
+      S = S + tsum[64 + tid];
+      float pp = (0.5f * S) + c0p;
+      if (amh_isnan(pp)) pp = INFINITY;
+      const float ex = amh_expf(pe_c - pp);
+      a = (ex > 1.0f) ? 1.0f : ex;
+      acc_f = uu[tid] < a;
+      p.pe_out[c0 + tid] = acc_f ? pp : pe_c;
+    }
+    flag[tid] = acc_f;
+    alph[tid] = a;
+  }
+  __syncthreads();
+  // (5) z' out, delta = z' - mu in place of z (k-major)
+  static_for<16>([&](auto N) {
+    const int cc = w + 4 * N;
+    float dv = 0.0f;
+    if (cc < nv) {
+      const float zn = flag[cc] ? Xb[lane * kFLd + cc] : Zb[lane * kFLd + cc];
+      p.z_out[(c0 + cc) * d + lane] = zn;
+      dv = zn - mu_l;
+    }
+    Zb[lane * kFLd + cc] = dv;
+  });
+  __syncthreads();
+  // (6) the chunk's sums: S_d, S_a sequential over chains, S_dd on MFMA
+  double* out = p.partials + chunk * V;
+  if (tid < d) {
+    float sd = 0.0f;
+    for (int c = 0; c < nv; ++c) sd = sd + Zb[tid * kFLd + c];
+    out[tid] = (double)sd;
+  }
+  if (tid == 64) {
+    float sa = 0.0f;
+    for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+    out[d + P] = (double)sa;
+    out[d + P + 1] = (double)nv;
+  }
+#ifndef AMH_F64_NOSDD
+  if (w < 3) {
+#else
+  if (w < 0) {
+#endif
+    const int pI = (w == 0) ? 0 : 1, pJ = (w == 2) ? 1 : 0;
+    const int ra = (32 * pI + i) * kFLd, rb = (32 * pJ + i) * kFLd;
+    f32x16 sacc = f32x16{};
+    int kk = 0;
+    for (; kk + 16 <= nv; kk += 16) {
+      float a[8], b[8];
+      static_for<8>([&](auto Q) {
+        a[Q] = Zb[ra + kk + 2 * Q + h];
+        b[Q] = Zb[rb + kk + 2 * Q + h];
+      });
+      static_for<8>([&](auto Q) { sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], sacc, 0, 0, 0); });
+    }
+    for (; kk < nv; kk += 2) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(Zb[ra + kk + h], Zb[rb + kk + h], sacc, 0, 0, 0);
+    static_for<16>([&](auto R) {
+      const int row = 32 * pI + (R & 3) + 8 * (R >> 2) + 4 * h;
+      const int col = 32 * pJ + i;
+      if (row >= col) out[d + pk(d, row, col)] = (double)sacc[(int)R];
+    });
+  }
+  }  // chunks
 }
 
 // ------------------------------------------------------------------ update --
@@ -544,11 +748,27 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
                          hipStream_t s);
 
-int64_t pooled_big_chunks(int64_t C) { return (C + kBigChunk - 1) / kBigChunk; }
+// chains per chunk of the sums (bit spec): 64 at d = 64 (the fused kernel's
+// block), 256 above
+int64_t pooled_big_chunks(int64_t C, int d) {
+  const int64_t ch = (d == kF) ? kFChunk : kBigChunk;
+  return (C + ch - 1) / ch;
+}
 
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s) {
   const int d = p.d;
   const int64_t V = d + (int64_t)d * (d + 1) / 2 + 2;
+  if (d == kF) {  // one launch (+ the reduction) per step
+    const int64_t nch = pooled_big_chunks(p.C, d);
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = nch < 2 * (int64_t)cus ? nch : 2 * (int64_t)cus;  // persistent: P, L staged once per block
+    hipLaunchKernelGGL(pooled_fused64_kernel, dim3((unsigned)grid), dim3(256), fused64_lds_bytes(), s, p, nch);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return pooled_reduce(p.partials, nch, V, sums, p.accumulate, s);
+  }
   hipLaunchKernelGGL(pooled_big_propose_kernel, dim3((unsigned)((p.C + 63) / 64)), dim3(256),
                      (size_t)d * kLd * sizeof(float), s, p, xprop);
   hipError_t e = hipGetLastError();
@@ -556,7 +776,7 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
   PotParams q{xprop, pep, p.C, d, p.model};
   e = run_big_potential(q, s);
   if (e != hipSuccess) return e;
-  const int64_t nch = pooled_big_chunks(p.C);
+  const int64_t nch = pooled_big_chunks(p.C, d);
   // split each chunk's tile pairs over enough blocks to cover the CUs
   const int nt = d / 32, npairs = nt * (nt + 1) / 2;
   int split = (int)((256 + nch - 1) / nch);

@@ -503,11 +503,12 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
   const int d = h->cfg.dim;
-  const bool big = amh::big_model(h->model_id, d);
+  const bool big = amh::pooled_big_model(h->model_id, d);
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
-  const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains) : (num_chains + chunk - 1) / chunk;
-  const size_t need = (size_t)n_chunks * (size_t)(d + (int64_t)d * (d + 1) / 2 + 2) * sizeof(double);
+  const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains, d) : (num_chains + chunk - 1) / chunk;
+  const size_t need = (size_t)amh::pooled_scratch_rows(n_chunks) * (size_t)(d + (int64_t)d * (d + 1) / 2 + 2) *
+                      sizeof(double);
   if (need > h->partials_bytes) {
     if (h->partials) {
       (void)hipStreamSynchronize((hipStream_t)stream);  // a queued launch may still use the old scratch
@@ -550,7 +551,7 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
       }
       e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
                                     (hipStream_t)stream);
-      if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(d > 64)");
+      if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(MFMA path)");
     }
     return AMH_OK;
   }
@@ -581,7 +582,7 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
   p.in = *in;
   p.out = *out;
   p.K = k_steps;
-  if (p.d > 64) {
+  if (amh::pooled_big_model(h->model_id, p.d)) {
     const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 4) * sizeof(float);
     int rc = grow(h, &h->upd_buf, &h->upd_bytes, need, stream, "amh_pooled_update/hipMalloc");
     if (rc != AMH_OK) return rc;

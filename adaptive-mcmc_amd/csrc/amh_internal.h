@@ -119,7 +119,8 @@ struct PooledUpdateParams {
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);
 // large dimensions (amh_big_pooled.hip): chunks of 256 chains
-int64_t pooled_big_chunks(int64_t C);
+int64_t pooled_big_chunks(int64_t C, int d);
+int64_t pooled_scratch_rows(int64_t n_chunks);  // partials + group sums of pooled_reduce
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);
 hipError_t run_asss_step(int model_id, const StepParams& p, hipStream_t s);  // amh_asss.hip
@@ -154,6 +155,7 @@ struct BigParams {
   float* col_pe;           // [C] or null
 };
 bool big_model(int model_id, int d);
+bool pooled_big_model(int model_id, int d);
 hipError_t run_big_init(const InitParams& p, hipStream_t s);
 hipError_t run_big_propose(const BigParams& p, hipStream_t s);
 // next: also form the next transition's proposal and solves (multi-step launches)

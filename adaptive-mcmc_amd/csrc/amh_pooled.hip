@@ -218,40 +218,57 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
 
 // Chunk partials -> sums, in a fixed two-level order (oracle mirror):
 // groups of kRedGroup consecutive chunks are summed in chunk order, then the
-// group sums in group order.  Block (v-slice, 16 x 64 threads): thread
-// (grp-lane q, v) sums groups q, q + 16, ... ; one thread per v then adds
-// the group sums in group order.
+// group sums in group order.  Two launches, each with a thread per (group, v)
+// or per v: pooled_group_kernel writes the group sums after the partials
+// (the scratch holds n_chunks + n_groups rows of V doubles), and
+// pooled_final_kernel adds them in group order.
 constexpr int kRedGroup = 16;
 
-__global__ __launch_bounds__(1024) void pooled_reduce_kernel(const double* partials, int64_t n_chunks, int64_t V,
-                                                             double* sums, int accumulate) {
-  __shared__ double gs[16][64];
-  const int tv = threadIdx.x & 63;
-  const int q = threadIdx.x >> 6;
-  const int64_t v = (int64_t)blockIdx.x * 64 + tv;
-  const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
-  double tot = 0.0;
-  for (int64_t g0 = 0; g0 < n_groups; g0 += 16) {
-    const int64_t g = g0 + q;
-    double s = 0.0;
-    if (v < V && g < n_groups) {
-      const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
-      for (int64_t ch = g * kRedGroup; ch < c1; ++ch) s += partials[ch * V + v];
-    }
-    gs[q][tv] = s;
-    __syncthreads();
-    if (q == 0 && v < V) {
-      for (int k = 0; k < 16 && g0 + k < n_groups; ++k) tot += gs[k][tv];
-    }
-    __syncthreads();
-  }
-  if (q == 0 && v < V) sums[v] = accumulate ? sums[v] + tot : tot;
+__global__ __launch_bounds__(256) void pooled_group_kernel(const double* __restrict__ partials, int64_t n_chunks,
+                                                           int64_t V, double* __restrict__ gsum) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t g = blockIdx.y;
+  if (v >= V) return;
+  const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
+  double x[kRedGroup];
+#pragma unroll
+  for (int q = 0; q < kRedGroup; ++q) x[q] = (g * kRedGroup + q < c1) ? partials[(g * kRedGroup + q) * V + v] : 0.0;
+  double s = 0.0;  // chunk order; a missing tail chunk adds nothing (it is not added at all)
+#pragma unroll
+  for (int q = 0; q < kRedGroup; ++q)
+    if (g * kRedGroup + q < c1) s += x[q];
+  gsum[g * V + v] = s;
 }
+
+__global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
+                                                           double* sums, int accumulate) {
+  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (v >= V) return;
+  double tot = 0.0;
+  int64_t g = 0;
+  for (; g + 8 <= n_groups; g += 8) {  // loads in flight, adds in group order
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = gsum[(g + q) * V + v];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tot += x[q];
+  }
+  for (; g < n_groups; ++g) tot += gsum[g * V + v];
+  sums[v] = accumulate ? sums[v] + tot : tot;
+}
+
+int64_t pooled_scratch_rows(int64_t n_chunks) { return n_chunks + (n_chunks + kRedGroup - 1) / kRedGroup; }
 
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
                          hipStream_t s) {
-  hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, partials, n_chunks, V,
-                     sums, accumulate);
+  const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
+  double* gsum = const_cast<double*>(partials) + n_chunks * V;
+  const unsigned vb = (unsigned)((V + 255) / 256);
+  hipLaunchKernelGGL(pooled_group_kernel, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials, n_chunks, V, gsum);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pooled_final_kernel, dim3(vb), dim3(256), 0, s, (const double*)gsum, n_groups, V, sums,
+                     accumulate);
   return hipGetLastError();
 }
 
@@ -406,9 +423,7 @@ hipError_t launch_pooled_stats(const PooledStatsParams& p, double* sums, hipStre
   hipLaunchKernelGGL((pooled_stats_kernel<M, EXACT>), dim3((unsigned)n_chunks), dim3(kPoolWaves * 64), shm, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pooled_reduce_kernel, dim3((unsigned)((V + 63) / 64)), dim3(1024), 0, s, p.partials,
-                     n_chunks, V, sums, 0);
-  return hipGetLastError();
+  return pooled_reduce(p.partials, n_chunks, V, sums, 0, s);
 }
 
 namespace {

@@ -658,6 +658,7 @@ int orc_num_threads(void) {
  * sums layout (V = d + P + 2 doubles): [S_d (d) | S_dd packed col-major (P) |
  * S_a | N]. */
 #define ORC_POOLED_WAVES 16
+#define ORC_BIG_D 256
 
 int orc_pooled_cpw(int64_t C) {
   const int64_t c = (C + 4095) / 4096;
@@ -683,16 +684,22 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
 static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t K, int32_t* i_, float* macc,
                                  float* mu, float* Lpacked, float* lam, float* asc, double* cov);
 
+/* The MFMA path of the pooled mode (amh_big_pooled.hip): the dense Gaussian
+ * with d % 32 == 0, 64 <= d <= 256 (amh_internal.h pooled_big_model). */
+static int orc_pooled_big(const orc_cfg* cfg) {
+  return cfg->model_id == ORC_GAUSSIAN && cfg->d >= 64 && cfg->d <= ORC_BIG_D && cfg->d % 32 == 0;
+}
+
 /* Pool every K (amh_pooled_stats_k): K transitions per chain with the frozen
  * shared state at noise positions i .. i+K-1, the sums over all K*C
- * chain-steps.  d <= 64: one kernel, each wave's chains in order with each
- * chain's K steps in order.  d > 64: K launch sequences, sums accumulated
+ * chain-steps.  Lane-per-row path: one kernel, each wave's chains in order
+ * with each chain's K steps in order.  MFMA path: K launch sequences, sums accumulated
  * in step order (sums = s_0, then sums + s_t). */
 void orc_pooled_stats_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, const float* z, const float* pe,
                         const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
                         float* z_out, float* pe_out, double* sums) {
   const int d = cfg->d;
-  if (d > ORC_DMAX) {
+  if (orc_pooled_big(cfg)) {
     const int64_t V = d + packed_size(d) + 2;
     double* tmp = (double*)malloc((size_t)V * sizeof(double));
     for (int32_t t = 0; t < K; ++t) {
@@ -812,7 +819,7 @@ static int32_t orc_block_n(int32_t it, int32_t W, int32_t K) { return (it < W) ?
 int orc_pooled_update_k(const orc_cfg* cfg, const double* sums, int32_t K, int32_t* i_, float* macc, float* mu,
                         float* Lpacked, float* lam, float* asc, double* cov) {
   const int d = cfg->d;
-  if (d > ORC_DMAX) return orc_pooled_update_big(cfg, sums, K, i_, macc, mu, Lpacked, lam, asc, cov);
+  if (orc_pooled_big(cfg)) return orc_pooled_update_big(cfg, sums, K, i_, macc, mu, Lpacked, lam, asc, cov);
   const int64_t P = packed_size(d);
   const double N = sums[d + P + 1];
   const int32_t it = *i_;
@@ -1107,14 +1114,15 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
  *  proposal  z' = z + fmaf(e^lam, acc, eps xi), acc_r = fmaf chain over
  *            k < 32 (floor(r / 32) + 1) of L_rk xi_k (L_rk = 0 above the
  *            diagonal; MFMA on 32-row tiles), U(z') in the MFMA order.
- *  sums      chunks of 256 consecutive chains: float32 S_dd (fmaf chain over
+ *  sums      chunks of 256 (d = 64: 64) consecutive chains: float32 S_dd (fmaf chain over
  *            the chunk's chains in order, MFMA), S_d and S_a (sequential
  *            adds), written in double; chunks reduced as in the d <= 64 mode.
  *  update    Sigma' in double as the d <= 64 mode; its Cholesky factor in
  *            float32 (element (r, k) updated in column order j < k, then
  *            divided by L_kk = sqrtf(A_kk)); as_change per row sequential,
  *            rows by big_sum. */
-#define ORC_BIG_CHUNK 256
+/* chains per chunk: 64 at d = 64 (pooled_fused64_kernel), 256 above */
+static int64_t orc_big_chunk(int d) { return d == 64 ? 64 : 256; }
 
 static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
                                  const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
@@ -1122,7 +1130,8 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
   const int d = cfg->d;
   const int64_t P = packed_size(d);
   const int64_t V = d + P + 2;
-  const int64_t n_chunks = (C + ORC_BIG_CHUNK - 1) / ORC_BIG_CHUNK;
+  const int64_t chunk = orc_big_chunk(d);
+  const int64_t n_chunks = (C + chunk - 1) / chunk;
   const float el = amh_expf(lam);
   double* part = (double*)calloc((size_t)(n_chunks * V), sizeof(double));
 #pragma omp parallel for schedule(dynamic, 1)
@@ -1132,7 +1141,7 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
     float sa = 0.0f;
     double cnt = 0.0;
     for (int r = 0; r < d; ++r) sd[r] = 0.0f;
-    for (int64_t c = ch * ORC_BIG_CHUNK; c < C && c < (ch + 1) * ORC_BIG_CHUNK; ++c) {
+    for (int64_t c = ch * chunk; c < C && c < (ch + 1) * chunk; ++c) {
       cnt += 1.0;
       const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
       uint32_t ubits = 0;
