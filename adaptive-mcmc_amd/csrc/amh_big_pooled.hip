@@ -597,41 +597,39 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
     }
     __syncthreads();
     US(2)
-    // (3) trailing update with the panel's 32 columns: 8x8 element tiles,
-    // packed FMAs (each lane of v_pk_fma_f32 is an fmaf), column j's 8 rows as
-    // two aligned 16-B reads
-    const int nb = (d - q0) / 8;
-    for (int tix = tid; tix < nb * (nb + 1) / 2; tix += 1024) {
-      int R = (int)((sqrtf(8.0f * (float)tix + 1.0f) - 1.0f) * 0.5f);
-      while (R * (R + 1) / 2 > tix) --R;
-      while ((R + 1) * (R + 2) / 2 <= tix) ++R;
-      const int Cb = tix - R * (R + 1) / 2;
-      const int r0 = q0 + 8 * R, c0 = q0 + 8 * Cb;
-      f32x2 t[8][4];
-      static_for<8>([&](auto Y) {
-        const int cbase = a4_base(d, c0 + Y) + r0;
-        static_for<8>([&](auto X) { t[X][(int)Y / 2][(int)Y % 2] = A[cbase + X]; });
-      });
-      int cb = a4_base(d, p0);
-      for (int j = 0; j < 32; ++j) {
-        const f32x4 r4a = *(const f32x4*)&A[cb + r0], r4b = *(const f32x4*)&A[cb + r0 + 4];
-        const f32x4 c4a = *(const f32x4*)&A[cb + c0], c4b = *(const f32x4*)&A[cb + c0 + 4];
-        const float lr[8] = {r4a[0], r4a[1], r4a[2], r4a[3], r4b[0], r4b[1], r4b[2], r4b[3]};
-        const f32x2 lc[4] = {f32x2{c4a[0], c4a[1]}, f32x2{c4a[2], c4a[3]}, f32x2{c4b[0], c4b[1]},
-                             f32x2{c4b[2], c4b[3]}};
-        static_for<8>([&](auto X) {
-          const f32x2 nl = f32x2{-lr[X], -lr[X]};
-          static_for<4>([&](auto Y) { t[X][Y] = __builtin_elementwise_fma(nl, lc[Y], t[X][Y]); });
+    // (3) trailing update with the panel's 32 columns on MFMA: each wave
+    // takes 32x32 tile pairs (I >= J) of the trailing matrix, acc = A_IJ and
+    // 16 v_mfma_f32_32x32x2_f32 with A = -L_I (rows x panel columns) and
+    // B = L_J^T -- per element the fmaf chain fmaf(-L_rj, L_cj, .) over
+    // j = 0..31 in order, the bits of the VALU form it replaces.
+    {
+      const int mt = (d - q0) / 32;
+      const int npair = mt * (mt + 1) / 2;
+      const int hh = lane >> 5, ii = lane & 31;
+      for (int pp = w; pp < npair; pp += 16) {
+        int I = 0;
+        while ((I + 1) * (I + 2) / 2 <= pp) ++I;
+        const int J = pp - I * (I + 1) / 2;
+        const int rI = q0 + 32 * I, cJ = q0 + 32 * J;
+        f32x16 acc;
+        const int col = cJ + ii;
+        const int cb = a4_base(d, col);
+        static_for<16>([&](auto R) {
+          const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
+          acc[(int)R] = (row >= (col & ~3)) ? A[cb + row] : 0.0f;
         });
-        cb += d - ((p0 + j + 1) & ~3);  // a4_base(d, p0 + j + 1)
+        static_for<16>([&](auto K2) {
+          const int k = p0 + 2 * K2 + hh;
+          const int kb = a4_base(d, k);
+          const float av = -A[kb + rI + ii];
+          const float bv = A[kb + cJ + ii];
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+        });
+        static_for<16>([&](auto R) {
+          const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
+          if (row >= col) A[cb + row] = acc[(int)R];
+        });
       }
-      static_for<8>([&](auto Y) {
-        const int c = c0 + Y;
-        const int cbase = a4_base(d, c) + r0;
-        static_for<8>([&](auto X) {
-          if (c <= r0 + X) A[cbase + X] = t[X][(int)Y / 2][(int)Y % 2];
-        });
-      });
     }
     __syncthreads();
     US(3)
