@@ -702,16 +702,26 @@ __global__ void chain_keys_kernel(uint32_t key0, uint32_t key1, int64_t offset, 
 //   ds_read_b128, in place of v_readlane + s_nop per column.  Only sweep 1,
 //   whose w_j is serial, still uses v_readlane.
 #ifndef AMH_S64_WAVES
-#define AMH_S64_WAVES 12
+#define AMH_S64_WAVES 16
 #endif
 constexpr int kS64Waves = AMH_S64_WAVES;
+#ifndef AMH_S64_EB
+#define AMH_S64_EB 8
+#endif
+#ifndef AMH_S64_PB
+#define AMH_S64_PB 8
+#endif
+constexpr int kS64EB = AMH_S64_EB;  // proposal: broadcast columns per LDS wait (16 or 8)
+constexpr int kS64PB = AMH_S64_PB;  // potential: columns per LDS wait (16 or 8)
+static_assert((kS64EB == 16 || kS64EB == 8) && (kS64PB == 16 || kS64PB == 8), "batch sizes");
 typedef uint32_t uint32x4_t_ __attribute__((ext_vector_type(4)));
 constexpr int kS64P = 2080;                   // d(d+1)/2
 constexpr int kS64Z = 2080, kS64M = 2144, kS64S = 2208, kS64X = 2216;  // wave-buffer offsets (floats)
-constexpr int kS64WB = kS64X + 256;           // floats per wave buffer (9,888 B)
+constexpr int kS64WB = kS64X + 64;            // floats per wave buffer (9,120 B): 64-float scratch
 constexpr int kS64Model = 64 * 68;            // GaussianM<64> rows (lds_bytes / 4)
 static_assert(kS64Z == 2080 && kS64S == kS64M + 64, "layout of prefetch_item<64>");
-constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)kS64Waves * kS64WB + 4) * sizeof(float); }
+// + 32 floats: the ticket, and slack for flush_factor's 9 KiB read of the last wave buffer
+constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)kS64Waves * kS64WB + 32) * sizeof(float); }
 
 constexpr int s64_col(int j) { return j * 64 - j * (j - 1) / 2; }  // packed column offset
 #ifdef AMH_S64_NOP
@@ -754,6 +764,15 @@ __device__ __forceinline__ void s64_sweep1(float& w, float u) {
                "v_fma_f32 %0, -%1, %3, %0\n\ts_mov_b64 exec, %2"
                : "+v"(w), "=&s"(t), "=&s"(sv) : "v"(u), "n"(J), "n"(J + 1));
 }
+// lanes 16Q .. 16Q+15 write v0..v3 at a, a+64, a+128, a+192 (a = scratch + 4 (r mod 16))
+template <int Q>
+__device__ __forceinline__ void s64_wr4_quarter(uint32_t a, float v0, float v1, float v2, float v3) {
+  uint64_t sv;
+  asm volatile("s_mov_b64 %0, exec\n\ts_bfm_b64 exec, 16, %6\n\tds_write_b32 %1, %2\n\t"
+               "ds_write_b32 %1, %3 offset:64\n\tds_write_b32 %1, %4 offset:128\n\t"
+               "ds_write_b32 %1, %5 offset:192\n\ts_mov_b64 exec, %0"
+               : "=&s"(sv) : "v"(a), "v"(v0), "v"(v1), "v"(v2), "v"(v3), "n"(16 * Q) : "memory");
+}
 __device__ __forceinline__ void s64_wr(uint32_t a, float v) {  // this lane's dword at a
   asm volatile("ds_write_b32 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
@@ -785,7 +804,9 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   const int wave_in_block = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
   float* wb = lds + kS64Model + wave_in_block * kS64WB;
   const uint32_t wb_a = lds_addr(wb);
-  const uint32_t x_a = wb_a + kS64X * 4;            // scratch (broadcast vectors)
+  const uint32_t x_a = wb_a + kS64X * 4;            // scratch (64 floats: broadcast vectors)
+  const uint32_t zm_a = wb_a + kS64Z * 4;           // z / loc region (swap vectors once read)
+  const uint32_t xq_a = x_a + (uint32_t)(lane_id() & 15) * 4u;  // sweep-2 quarter slot
   const uint32_t prow = lds_addr(lds) + (uint32_t)lane_id() * (uint32_t)(M::ld(D) * 4);  // row r of P
 
   float U[D];  // row r of U = L / diag(L): unit diagonal, zeros above (kept between chains)
@@ -846,6 +867,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   auto flush_factor = [&](int64_t c) {
     const Buf Lout(uniform_ptr(p.out.scale + c * P), P * 4u);
     const uint32_t la = wb_a + (uint32_t)lane_id() * 16u;
+#ifdef AMH_S64_FLUSH9
     f32x4 v[9];
     v[0] = lds_ld4<0>(la); v[1] = lds_ld4<1024>(la); v[2] = lds_ld4<2048>(la);
     v[3] = lds_ld4<3072>(la); v[4] = lds_ld4<4096>(la); v[5] = lds_ld4<5120>(la);
@@ -856,6 +878,18 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32x4_t_, v[(int)Q]), Lout.rs,
                                              (int)(1024u * Q + 16u * (uint32_t)lane_id()), 0, AMH_STORE_AUX);
     });
+#else
+    static_for<3>([&](auto G) {  // three dwordx4 per lane in flight per wait
+      f32x4 v[3];
+      static_for<3>([&](auto Q) { v[(int)Q] = lds_ld4<1024 * (3 * G + Q)>(la); });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]));
+      static_for<3>([&](auto Q) {
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32x4_t_, v[(int)Q]), Lout.rs,
+                                               (int)(1024u * (3 * G + Q) + 16u * (uint32_t)lane_id()), 0,
+                                               AMH_STORE_AUX);
+      });
+    });
+#endif
   };
 
   int64_t item = ticket();
@@ -873,35 +907,10 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     const bool wr = prev >= 0 && prev_upd;
     if (prev >= 0 && !prev_upd) copy_verbatim(prev, r);
 
-    // ---- diagonal of item k; broadcast vectors [dl of k-1 | 1 / l of k]
+    // ---- diagonal of item k
     float lnew = lds_ld1<0>(wb_a + (uint32_t)s64_col(r) * 4u);
     s64_tie(lnew);
     const float inv = (amh_isfinite(lnew) && lnew != 0.0f) ? 1.0f / lnew : 0.0f;
-    s64_wr(x_a + (uint32_t)r * 4u, dl);
-    s64_wr_off<256>(x_a + (uint32_t)r * 4u, inv);
-
-    // ---- swap: read item k's column j (lanes > j), write item k-1's column j
-    //      of L' = U diag(dl) (lanes >= j) at the same addresses, normalise
-    static_for<16>([&](auto G4) {
-      constexpr int g = G4;
-      f32x4 dl4 = lds_ld4<16 * g>(x_a);
-      f32x4 in4 = lds_ld4<256 + 16 * g>(x_a);
-      s64_tie(dl4, in4);
-      float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      static_for<4>([&](auto Q) {
-        constexpr int j = 4 * g + Q;
-        constexpr int off = (s64_col(j) - j) * 4;
-        if constexpr (j < D - 1) s64_rd_above<j, off>(t[(int)Q], la);
-        if (wr) s64_wr_from<j, off>(la, U[j] * dl4[(int)Q]);
-      });
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]));
-      static_for<4>([&](auto Q) {
-        constexpr int j = 4 * g + Q;
-        if constexpr (j < D - 1) s64_mul_above<j>(U[j], t[(int)Q], in4[(int)Q]);
-      });
-    });
-    if (wr) flush_factor(prev);
-
     // ---- item k's z / loc / scalars: LDS -> registers
     {
       float zz = lds_ld1<kS64Z * 4>(la), mm = lds_ld1<kS64M * 4>(la);
@@ -919,9 +928,35 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       asc = s4v;
       k0 = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s5));
       k1 = (uint32_t)__builtin_amdgcn_readfirstlane(__float_as_int(s6));
+      // broadcast vectors [dl of k-1 | 1 / l of k] over item k's z / loc, now in registers
+      s64_wr(zm_a + (uint32_t)r * 4u, dl);
+      s64_wr_off<256>(zm_a + (uint32_t)r * 4u, inv);
       dl = lnew;
       acc0 = (p.accept_count != nullptr && r == 0) ? p.accept_count[item] : 0;
     }
+
+    // ---- swap: read item k's column j (lanes > j), write item k-1's column j
+    //      of L' = U diag(dl) (lanes >= j) at the same addresses, normalise
+    static_for<16>([&](auto G4) {
+      constexpr int g = G4;
+      f32x4 dl4 = lds_ld4<16 * g>(zm_a);
+      f32x4 in4 = lds_ld4<256 + 16 * g>(zm_a);
+      s64_tie(dl4, in4);
+      float t[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      static_for<4>([&](auto Q) {
+        constexpr int j = 4 * g + Q;
+        constexpr int off = (s64_col(j) - j) * 4;
+        if constexpr (j < D - 1) s64_rd_above<j, off>(t[(int)Q], la);
+        if (wr) s64_wr_from<j, off>(la, U[j] * dl4[(int)Q]);
+      });
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3]));
+      static_for<4>([&](auto Q) {
+        constexpr int j = 4 * g + Q;
+        if constexpr (j < D - 1) s64_mul_above<j>(U[j], t[(int)Q], in4[(int)Q]);
+      });
+    });
+    if (wr) flush_factor(prev);
+
     s64_wait();  // every LDS read of the buffer is done before the DMA refills it
     int64_t nxt2 = blk_hi;
     if (nxt < blk_hi) {
@@ -944,20 +979,21 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       s64_wr(x_a + (uint32_t)r * 4u, eta);
 #endif
       float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      static_for<4>([&](auto B) {  // 16 columns per batch
+      static_for<D / kS64EB>([&](auto B) {  // kS64EB columns per batch
         constexpr int b = B;
-        f32x4 e[4];
+        f32x4 e[kS64EB / 4];
 #ifndef AMH_S64_BC_RL
-        e[0] = lds_ld4<64 * b>(x_a);
-        e[1] = lds_ld4<64 * b + 16>(x_a);
-        e[2] = lds_ld4<64 * b + 32>(x_a);
-        e[3] = lds_ld4<64 * b + 48>(x_a);
-        lds_wait(e[0], e[1], e[2], e[3]);
+        static_for<kS64EB / 4>([&](auto Q) { e[(int)Q] = lds_ld4<16 * (kS64EB / 4 * b + Q)>(x_a); });
+        if constexpr (kS64EB == 16) {
+          lds_wait(e[0], e[1], e[2], e[3]);
+        } else {
+          s64_tie(e[0], e[1]);
+        }
 #else
-        static_for<16>([&](auto K) { e[(int)K / 4][(int)K % 4] = Gp::template bcast<16 * b + K>(eta); });
+        static_for<kS64EB>([&](auto K) { e[(int)K / 4][(int)K % 4] = Gp::template bcast<kS64EB * b + K>(eta); });
 #endif
-        static_for<16>([&](auto K) {
-          constexpr int j = 16 * b + K;
+        static_for<kS64EB>([&](auto K) {
+          constexpr int j = kS64EB * b + K;
           a4[j & 3] = fmaf(U[j], e[(int)K / 4][(int)K % 4], a4[j & 3]);
         });
         __builtin_amdgcn_sched_barrier(0);
@@ -973,20 +1009,25 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
         s64_wr(x_a + (uint32_t)r * 4u, diff);
 #endif
         f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
-        static_for<4>([&](auto B) {
+        static_for<D / kS64PB>([&](auto B) {
           constexpr int b = B;
-          f32x4 pv[4], dv[4];
-          static_for<4>([&](auto Q) {
-            pv[(int)Q] = lds_ld4<16 * (4 * b + Q)>(prow);
+          constexpr int NQ = kS64PB / 4;
+          f32x4 pv[NQ], dv[NQ];
+          static_for<NQ>([&](auto Q) {
+            pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
 #ifndef AMH_S64_BC_RL
-            dv[(int)Q] = lds_ld4<16 * (4 * b + Q)>(x_a);
+            dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
 #else
-            static_for<4>([&](auto K) { dv[(int)Q][(int)K] = Gp::template bcast<16 * b + 4 * Q + K>(diff); });
+            static_for<4>([&](auto K) { dv[(int)Q][(int)K] = Gp::template bcast<kS64PB * b + 4 * Q + K>(diff); });
 #endif
           });
-          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
-                       "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
-          static_for<8>([&](auto K2) {
+          if constexpr (NQ == 4) {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
+                         "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+          } else {
+            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+          }
+          static_for<2 * NQ>([&](auto K2) {
             const f32x4 q = pv[(int)K2 / 2];
             const f32x4 dq = dv[(int)K2 / 2];
             const f32x2v pp = (K2 % 2 == 0) ? f32x2v{q[0], q[1]} : f32x2v{q[2], q[3]};
@@ -1066,18 +1107,15 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
         //   U_rj (q_j e1 - dl_j e0) + (c_j q_j e1) w_r^{(j+1)}
         const float ac = (q * e1) - (dl * el);
         const float bc = (c * q) * e1;
-#ifndef AMH_S64_BC_RL
-        s64_wr(x_a + (uint32_t)r * 4u, ws);
-        s64_wr_off<256>(x_a + (uint32_t)r * 4u, c);
-        s64_wr_off<512>(x_a + (uint32_t)r * 4u, ac);
-        s64_wr_off<768>(x_a + (uint32_t)r * 4u, bc);
-#endif
         float w = delta;
         static_for<16>([&](auto G4) {
           constexpr int g = G4;
 #ifndef AMH_S64_BC_RL
-          f32x4 cw = lds_ld4<16 * g>(x_a), cc = lds_ld4<256 + 16 * g>(x_a);
-          f32x4 ca = lds_ld4<512 + 16 * g>(x_a), cb = lds_ld4<768 + 16 * g>(x_a);
+          // the four coefficient vectors of columns 16(g/4) .. +15 (lanes of that quarter write)
+          if constexpr (g % 4 == 0) s64_wr4_quarter<g / 4>(xq_a, ws, c, ac, bc);
+          constexpr int gq = g % 4;
+          f32x4 cw = lds_ld4<16 * gq>(x_a), cc = lds_ld4<64 + 16 * gq>(x_a);
+          f32x4 ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
           lds_wait(cw, cc, ca, cb);
 #else
           f32x4 cw, cc, ca, cb;
