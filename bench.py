@@ -79,6 +79,13 @@ def measured_traffic(C: int, d: int):
     return best
 
 
+def step_kernel_name(d: int) -> str:
+    """The kernel the headline leg launches (amh_kernels.hip run_step dispatch)."""
+    if d == 64 and os.environ.get("AMH_STEP64", "1") != "0":
+        return "arwmh_step64_kernel<16> (d = 64 specialisation, 16 waves/CU)"
+    return f"arwmh_step_kernel<{d}, GaussianM>"
+
+
 # ----------------------------------------------------------------- ranks --
 def _free_port() -> int:
     s = socket.socket()
@@ -378,7 +385,7 @@ def main():
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
                     "traffic_source": traffic[1] if traffic else None, "kernel_ms": r["kern_ms"],
-                    "kernel": "arwmh_step_kernel<64,GaussianM,true,0>",
+                    "kernel": step_kernel_name(d),
                     "algorithmic_bytes_per_launch": per_launch_bytes}
         fused = None
         if extra and not args.no_fused:
@@ -416,7 +423,8 @@ def main():
     achieved = flops / (stats_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel_ms": stats_ms,
-                "kernel": "pooled stats (amh_pooled_stats_k: transitions + chunk sums)",
+                "kernel": ("pooled_fused64_kernel (amh_pooled_stats_k: transitions + 64-chain chunk sums on MFMA)"
+                           if d == 64 else "pooled stats (amh_pooled_stats_k: transitions + chunk sums)"),
                 "algorithmic_flops_per_launch": flops}
     sub = {}
     if extra:

@@ -3,15 +3,17 @@
 Inputs (gpurun_out/prof_<tag>/): rocprofv3 --kernel-trace --stats of
 `bench.py --steps S --warmup W` and two --pmc passes (FETCH_SIZE,
 WRITE_SIZE) of `bench.py --steps S2 --warmup W2`.  The step-kernel launches
-of bench.py come in order: W warmup, S timed single-step launches, one fused
-50-step launch; only the timed ones are summarised.
+of bench.py come in order: W warmup, the clock-warm launches (a fixed wall
+time, so a variable count), S timed single-step launches, then (default
+command) one fused 50-step launch and the ESS leg's launches; the S launches
+before the first long (fused) launch are summarised.
 
 HBM traffic per launch (MI355X_MICROARCH.md, HBM section): FETCH_SIZE and
 WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE counts half the bytes of wide
 (16 B/lane) streaming reads -- the factor, 94 % of the bytes read here, is
 moved by 16 B/lane buffer_load...lds -- so it is doubled.
 
-  python tools/prof_summary.py r1 [--steps 100 --warmup 10 --pmc-steps 20 --pmc-warmup 2]
+  python tools/prof_summary.py r2 [--steps 200 --pmc-steps 20]
 """
 import argparse
 import csv
@@ -21,7 +23,7 @@ import shutil
 import statistics
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNEL = "arwmh_step_kernel<64, amh::GaussianM, true"  # prefix: later builds add template args
+KERNEL = "arwmh_step64_kernel"  # the d = 64 specialisation (amh_kernels.hip)
 
 
 def step_rows(path):
@@ -31,7 +33,7 @@ def step_rows(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tag")
-    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--pmc-steps", type=int, default=20)
     ap.add_argument("--pmc-warmup", type=int, default=2)
@@ -44,12 +46,15 @@ def main():
 
     tr = step_rows(os.path.join(src, "trace", "run_kernel_trace.csv"))
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-3 for r in tr]  # us
-    timed = dur[a.warmup:a.warmup + a.steps]
-    fused = dur[a.warmup + a.steps:]
+    # the timed launches end where the fused 50-step launch (if any) begins
+    med = statistics.median(dur)
+    long_ = [i for i, x in enumerate(dur) if x > 10 * med]
+    end = long_[0] if long_ else len(dur)
+    timed = dur[end - a.steps:end]
 
     def pmc(name):
         rows = step_rows(os.path.join(src, f"pmc_{name}", "pmc_counter_collection.csv"))
-        v = [float(r["Counter_Value"]) for r in rows][a.pmc_warmup:a.pmc_warmup + a.pmc_steps]
+        v = [float(r["Counter_Value"]) for r in rows][-a.pmc_steps:]
         return statistics.mean(v)
 
     fetch_kib, write_kib = pmc("FETCH_SIZE"), pmc("WRITE_SIZE")
@@ -59,13 +64,12 @@ def main():
     out = {
         "tag": a.tag,
         "kernel": next(iter(r["Kernel_Name"] for r in tr)),
-        "workload": f"bench.py single-step launches, {C} chains, d={d}",
+        "workload": f"bench.py single-step launches, {C} chains, d={d} (timed region, after the clock warm)",
         "launches_timed": len(timed),
         "avg_us": statistics.mean(timed),
         "median_us": statistics.median(timed),
         "min_us": min(timed),
         "max_us": max(timed),
-        "fused_launch_us": fused,
         "algorithmic_bytes_per_launch": 2 * alg_read,
         "achieved_GBps_at_avg": 2 * alg_read / (statistics.mean(timed) * 1e-6) / 1e9,
         "FETCH_SIZE_KiB_per_launch": fetch_kib,
