@@ -1,21 +1,21 @@
 // amh_big_pooled.hip -- pooled-covariance mode (regime B) for the Gaussian
 // with d % 32 == 0, 64 <= d <= 256: BASELINE config 4's headline (d = 256,
 // one shared factor for 32,768 chains) and config 5's per-GPU work (d = 64,
-// 65,536 chains, pooled_fused64_kernel).
+// 65,536 chains).
 //
 // With one shared L every per-chain product is a GEMM over chains, so the
 // three O(d^2) pieces run on MFMA (v_mfma_f32_32x32x2_f32, a k-ordered fmaf
-// chain -- bit-reproducible by the oracle):
+// chain -- bit-reproducible by the oracle), fused into one persistent kernel
+// per step:
 //
-//   pooled_big_propose_kernel  Z' = Z + e^lam (L Xi) + eps Xi for 64 chains
-//                              per block; Xi drawn straight into LDS
-//                              (arwmh.py:162-167), L read from L2
-//   gauss_pot_mfma_kernel      U(Z') (amh_big.hip)
-//   pooled_big_stats_kernel    accept (arwmh.py:173-178) and the chunk sums
-//                              S_d, S_a and S_dd = sum delta delta^T, the
-//                              latter as a K = chains MFMA over 32x32 tile
-//                              pairs of the lower triangle
-//   pooled_reduce_kernel       chunk partials -> sums (amh_pooled.hip)
+//   pooled_fused64_kernel      d = 64: proposal Z' = Z + e^lam (L Xi) + eps Xi
+//                              (arwmh.py:162-167), U(Z'), accept
+//                              (arwmh.py:173-178) and the chunk sums S_d, S_a,
+//                              S_dd = sum delta delta^T of a 64-chain chunk;
+//                              L and P staged in LDS
+//   pooled_pack_kernel +       d > 64: the same for 128-chain chunks, L and
+//   pooled_fused_big_kernel    P read from L2 in MFMA A-operand order
+//   pooled_reduce              chunk partials -> sums (amh_pooled.hip)
 //   pooled_big_update_kernel   Sigma' = (1-g) Sigma + g S_dd / N (double) and
 //                              its blocked Cholesky factor (float32, 32-column
 //                              panels, the matrix resident in LDS)
@@ -27,7 +27,6 @@ namespace amh {
 namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kLd = 65;          // LDS row stride of [k][chain] tiles
-constexpr int kBigChunk = 256;   // chains per stats block (bit spec)
 
 __device__ __forceinline__ float rdlane(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -35,224 +34,9 @@ __device__ __forceinline__ float rdlane(float v, int l) {
 __device__ __forceinline__ int64_t pk(int d, int r, int k) { return col_off(d, k) + (r - k); }
 }  // namespace
 
-// ----------------------------------------------------------------- propose --
-__global__ __launch_bounds__(256) void pooled_big_propose_kernel(PooledStatsParams p, float* xprop) {
-  extern __shared__ float lds[];
-  const int d = p.d;
-  const int nt = d / 32;
-  float* Xi = lds;  // [k][chain]: the noise, then e^lam L xi + eps xi
-  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
-  const float el = amh_expf(p.lam[0]);
-  const int64_t c0 = (int64_t)blockIdx.x * 64;
-  for (int idx = threadIdx.x; idx < 64 * d; idx += 256) {
-    const int cc = idx / d, k = idx - cc * d;
-    int64_t ch = c0 + cc;
-    if (ch >= p.C) ch = p.C - 1;
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)it, 0u, AMH_TAG_STEP, p.keys[2 * ch],
-                                          p.keys[2 * ch + 1]);
-    Xi[k * kLd + cc] = amh_normal_from_bits(o.v[0]);
-  }
-  __syncthreads();
-  const int lane = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
-  const int h = lane >> 5, i = lane & 31;
-  // wave w owns row tiles w and nt-1-w (equal triangular work)
-  f32x16 acc[2][2];
-  static_for<2>([&](auto I2) { static_for<2>([&](auto T) { acc[I2][T] = f32x16{}; }); });
-  constexpr int NB = 8;
-  static_for<2>([&](auto I2) {
-    const int tile = I2 == 0 ? w : nt - 1 - w;
-    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
-    if (own) {
-      const int row = 32 * tile + i;
-      const int kend = 32 * (tile + 1);
-      float an[NB];
-      auto load = [&](int kk0) {
-        static_for<NB>([&](auto S) {
-          const int col = kk0 + 2 * S + h;
-          an[S] = (row >= col) ? p.L[pk(d, row, col)] : 0.0f;
-        });
-      };
-      load(0);
-      for (int kk0 = 0; kk0 < kend; kk0 += 2 * NB) {
-        float a[NB];
-        static_for<NB>([&](auto S) { a[S] = an[S]; });
-        if (kk0 + 2 * NB < kend) load(kk0 + 2 * NB);
-        static_for<NB>([&](auto S) {
-          const int col = kk0 + 2 * S + h;
-          acc[I2][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[S], Xi[col * kLd + i], acc[I2][0], 0, 0, 0);
-          acc[I2][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[S], Xi[col * kLd + 32 + i], acc[I2][1], 0, 0, 0);
-        });
-      }
-    }
-  });
-  // every wave has read all of Xi: replace it by fmaf(e^lam, L xi, eps xi)
-  float v[2][2][16];
-  static_for<2>([&](auto I2) {
-    const int tile = I2 == 0 ? w : nt - 1 - w;
-    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
-    if (own) {
-      static_for<16>([&](auto R) {
-        const int rr = 32 * tile + (R & 3) + 8 * (R >> 2) + 4 * h;
-        v[I2][0][R] = fmaf(el, acc[I2][0][(int)R], p.eps * Xi[rr * kLd + i]);
-        v[I2][1][R] = fmaf(el, acc[I2][1][(int)R], p.eps * Xi[rr * kLd + 32 + i]);
-      });
-    }
-  });
-  __syncthreads();
-  static_for<2>([&](auto I2) {
-    const int tile = I2 == 0 ? w : nt - 1 - w;
-    const bool own = (I2 == 0) ? (w <= nt - 1 - w) : (nt - 1 - w > w);
-    if (own) {
-      static_for<16>([&](auto R) {
-        const int rr = 32 * tile + (R & 3) + 8 * (R >> 2) + 4 * h;
-        Xi[rr * kLd + i] = v[I2][0][R];
-        Xi[rr * kLd + 32 + i] = v[I2][1][R];
-      });
-    }
-  });
-  __syncthreads();
-  for (int idx = threadIdx.x; idx < 64 * d; idx += 256) {
-    const int cc = idx / d, k = idx - cc * d;
-    const int64_t ch = c0 + cc;
-    if (ch < p.C) xprop[ch * d + k] = p.z[ch * d + k] + Xi[k * kLd + cc];
-  }
-}
-
-// ------------------------------------------------------------------- stats --
-// 8 waves per block; a chunk's lower tile pairs (I >= J) of S_dd (36 at d =
-// 256) are split over `split` blocks (blockIdx.y) so that a run of few chunks
-// still fills the chip: block part q owns pairs [q * per, (q + 1) * per) and
-// wave w of it local pairs w, w + 8, ...  Every part recomputes the chunk's
-// accept flags and deltas (cheap); part 0 alone writes z', U', S_d, S_a and the
-// count.  The chunk's chains feed the MFMA K dimension in order, so the split
-// does not change any sum.
-__global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams p, const float* xprop,
-                                                               const float* pep, int per) {
-  extern __shared__ float lds[];
-  const int d = p.d;
-  const int nt = d / 32;
-  const int npairs = nt * (nt + 1) / 2;
-  const int64_t P = (int64_t)d * (d + 1) / 2;
-  const int64_t V = d + P + 2;
-  float* Dl = lds;                         // [d][kLd]
-  int* flag = (int*)(lds + (size_t)d * kLd);  // [64]
-  float* alph = lds + (size_t)d * kLd + 64;   // [64]
-  const int tid = threadIdx.x;
-  const int lane = lane_id();
-  const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
-  const int h = lane >> 5, i = lane & 31;
-  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
-  const int64_t base = (int64_t)blockIdx.x * kBigChunk;
-  const int part = blockIdx.y;
-  const bool writer = part == 0;
-  const int pair0 = part * per;
-  const int pair1 = (pair0 + per < npairs) ? pair0 + per : npairs;
-  float sd = 0.0f, sa = 0.0f;
-  int64_t cnt = 0;
-  f32x16 acc[5];
-  int pI[5], pJ[5];
-  bool own[5];
-  static_for<5>([&](auto S) {
-    acc[S] = f32x16{};
-    const int pp = pair0 + w + 8 * S;
-    own[S] = pp < pair1;
-    int I = 0;
-    while ((I + 1) * (I + 2) / 2 <= pp) ++I;
-    pI[S] = I;
-    pJ[S] = pp - I * (I + 1) / 2;
-  });
-  const int kk2 = tid & 255, half = tid >> 8;  // gather: two chains per pass, k = tid mod 256
-  for (int t = 0; t < kBigChunk / 64; ++t) {
-    const int64_t c0 = base + 64 * t;
-    const int64_t left = p.C - c0;
-    if (left <= 0) break;
-    const int nv = left < 64 ? (int)left : 64;
-    if (tid < 64) {
-      int acc_f = 0;
-      float a = 0.0f;
-      if (tid < nv) {
-        const int64_t c = c0 + tid;
-        const amh_u32x4 o = amh_philox4x32_10(0u, (uint32_t)it, 0u, AMH_TAG_STEP, p.keys[2 * c], p.keys[2 * c + 1]);
-        const float u = amh_unif01_from_bits(o.v[1]);
-        float pp = pep[c];
-        if (amh_isnan(pp)) pp = INFINITY;
-        const float pe = p.pe[c];
-        const float ex = amh_expf(pe - pp);
-        a = (ex > 1.0f) ? 1.0f : ex;
-        acc_f = u < a;
-        if (writer) p.pe_out[c] = acc_f ? pp : pe;
-      }
-      flag[tid] = acc_f;
-      alph[tid] = a;
-    }
-    __syncthreads();
-    if (kk2 < d) {
-      const float muk = p.mu[kk2];
-      for (int cp = 0; cp < 32; ++cp) {
-        const int cc = 2 * cp + half;
-        float dv = 0.0f;
-        if (cc < nv) {
-          const int64_t c = c0 + cc;
-          const float* src = flag[cc] ? xprop : p.z;
-          const float zn = src[c * d + kk2];
-          if (writer) p.z_out[c * d + kk2] = zn;
-          dv = zn - muk;
-        }
-        Dl[kk2 * kLd + cc] = dv;
-      }
-    }
-    __syncthreads();
-    if (writer) {
-      if (tid < d) {
-        for (int c = 0; c < nv; ++c) sd = sd + Dl[tid * kLd + c];
-      }
-      if (tid == 511) {
-        for (int c = 0; c < nv; ++c) sa = sa + alph[c];
-      }
-    }
-    cnt += nv;
-    static_for<5>([&](auto S) {
-      if (own[S]) {
-        const int ra = (32 * pI[S] + i) * kLd, rb = (32 * pJ[S] + i) * kLd;
-        int kk = 0;
-        for (; kk + 16 <= nv; kk += 16) {
-          float a[8], b[8];
-          static_for<8>([&](auto Q) {
-            a[Q] = Dl[ra + kk + 2 * Q + h];
-            b[Q] = Dl[rb + kk + 2 * Q + h];
-          });
-          static_for<8>([&](auto Q) { acc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], acc[S], 0, 0, 0); });
-        }
-        for (; kk < nv; kk += 2) {
-          acc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(Dl[ra + kk + h], Dl[rb + kk + h], acc[S], 0, 0, 0);
-        }
-      }
-    });
-    __syncthreads();
-  }
-  double* out = p.partials + (int64_t)blockIdx.x * V;
-  if (writer) {
-    if (tid < d) out[tid] = (double)sd;
-    if (tid == 511) {
-      out[d + P] = (double)sa;
-      out[d + P + 1] = (double)cnt;
-    }
-  }
-  static_for<5>([&](auto S) {
-    if (own[S]) {
-      static_for<16>([&](auto R) {
-        const int row = 32 * pI[S] + (R & 3) + 8 * (R >> 2) + 4 * h;
-        const int col = 32 * pJ[S] + i;
-        if (row >= col) out[d + pk(d, row, col)] = (double)acc[S][(int)R];
-      });
-    }
-  });
-}
-
 // -------------------------------------------------- fused stats, d = 64 --
-// BASELINE configs[4]'s per-GPU work (d = 64, 65,536 chains): the three
-// launches above in one, one 64-chain chunk per 256-thread block (the chunk
+// BASELINE configs[4]'s per-GPU work (d = 64, 65,536 chains): proposal,
+// potential, accept and sums in one launch, one 64-chain chunk per 256-thread block (the chunk
 // size of the d = 64 bit spec; 1,024 blocks at the config, two resident per
 // CU), with the shared factor L and the precision P staged in LDS instead of
 // read from L2 per MFMA; the blocks are persistent (two per CU) and walk the
@@ -261,8 +45,8 @@ __global__ __launch_bounds__(512) void pooled_big_stats_kernel(PooledStatsParams
 // U(xprop) on MFMA with D = xprop - m formed as the B operand is read;
 // accept; delta = z' - mu in place of z; S_d, S_a sequential and S_dd on MFMA
 // (waves 0..2: tile pairs (0,0), (1,0), (1,1)).  Every float operation and
-// its order are those of pooled_big_propose_kernel + gauss_pot_mfma_kernel +
-// pooled_big_stats_kernel (oracle: orc_pooled_stats_big).
+// its order are those of pooled_fused_big_kernel at d = 64 (oracle:
+// orc_pooled_stats_big).
 constexpr int kF = 64;      // d
 constexpr int kFLd = 65;    // LDS row stride
 constexpr int kFChunk = 64; // chains per chunk at d = 64 (bit spec)
@@ -451,6 +235,346 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     });
   }
   }  // chunks
+}
+
+// --------------------------------------------------- fused stats, d > 64 --
+// BASELINE configs[3] regime B (d = 256, 32,768 chains) and every pooled
+// d = 32 NT > 64: proposal, potential, accept and the chunk sums in one
+// persistent 512-thread block per CU (8 waves, 2 per SIMD: 256 registers for
+// the S_dd accumulators that live across the chunk), a 128-chain chunk (the
+// bit spec's chunk above d = 64) in two 64-chain halves.  The MFMA A operands (the
+// shared factor's lower tiles and the precision's tiles) come from a
+// per-launch copy in "A-operand order" (pooled_pack_kernel): lane (i, h)
+// reads one 16-B vector = rows 32T + i, columns 32J + 8kb + 2e + h, e = 0..3,
+// i.e. four consecutive v_mfma_f32_32x32x2_f32 -- the tile's 16 MFMAs are 4
+// coalesced dwordx4 loads per lane, double-buffered one tile ahead.  The B
+// operands (noise, D = xprop - m, delta) are [k][chain] tiles in LDS.
+// Work split, per 64 chains (MFMA counts): proposal 16 NT(NT+1), wave w one
+// row tile for both chain halves (at NT = 8 the waves w, w+4 that share a
+// SIMD take tiles 7-w and w: equal sums per SIMD); potential 32 NT^2, wave w
+// row tile w; S_dd 16 NT(NT+1) in NT(NT+1)/2 tile pairs (wave w: pairs w,
+// w+8, .., accumulated over the chunk's 128 chains).  Partials are written
+// in "tile" order (coalesced; pooled_final_kernel maps them to the packed
+// sums).  Float operations and their
+// order: those of orc_pooled_stats_big (the MFMA k order of
+// gauss_pot_mfma_kernel for the potential).
+constexpr int kFB = 128;  // chains per chunk above d = 64 (bit spec)
+constexpr int kFBWaves = 8;
+template <int NT>
+constexpr size_t fused_big_lds_bytes() {
+  return ((size_t)2 * 32 * NT * kLd + (size_t)NT * 64 + 3 * 64 + 32 * NT) * sizeof(float);
+}
+int64_t pooled_big_tile_V(int d) {
+  const int nt = d / 32;
+  return d + (int64_t)(nt * (nt + 1) / 2) * 1024 + 2;
+}
+int64_t pooled_big_pack_floats(int d) {
+  const int nt = d / 32;
+  return (int64_t)(nt * (nt + 1) / 2 + nt * nt) * 1024;
+}
+
+// one block per tile: lower tiles of L (zeros above the diagonal), then the
+// NT x NT tiles of the precision P (row-major in the model data)
+__global__ __launch_bounds__(256) void pooled_pack_kernel(const float* __restrict__ L, const float* __restrict__ Pm,
+                                                          int d, float* __restrict__ pack) {
+  const int nt = d / 32;
+  const int npair = nt * (nt + 1) / 2;
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;            // = kb * 64 + lane
+  const int lane = t & 63, kb = t >> 6;
+  const int i = lane & 31, h = lane >> 5;
+  f32x4 v;
+  if (b < npair) {
+    int T = 0;
+    while ((T + 1) * (T + 2) / 2 <= b) ++T;
+    const int J = b - T * (T + 1) / 2;
+    const int row = 32 * T + i;
+    static_for<4>([&](auto E) {
+      const int col = 32 * J + 8 * kb + 2 * E + h;
+      v[(int)E] = (col <= row) ? L[pk(d, row, col)] : 0.0f;
+    });
+  } else {
+    const int b2 = b - npair;
+    const int T = b2 / nt, J = b2 - T * nt;
+    const int row = 32 * T + i;
+    static_for<4>([&](auto E) { v[(int)E] = Pm[(int64_t)row * d + 32 * J + 8 * kb + 2 * E + h]; });
+  }
+  ((f32x4*)pack)[(int64_t)b * 256 + t] = v;
+}
+
+template <int NT>
+__global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams p, const float* __restrict__ pack,
+                                                               int64_t n_chunks) {
+  constexpr int D = 32 * NT;
+  constexpr int NPAIR = NT * (NT + 1) / 2;
+  constexpr int64_t V = D + (int64_t)NPAIR * 1024 + 2;  // "tile" partial row (pooled_final_kernel maps it)
+  constexpr int NS = (NPAIR + kFBWaves - 1) / kFBWaves;  // S_dd tile pairs per wave (<= 5)
+  constexpr int NQ = (D + 63) / 64;  // coordinates per lane in the chain-major phases
+  constexpr int CPW = 64 / kFBWaves;  // chains per wave in the chain-major phases
+  static_assert(CPW % 4 == 0, "chain-major phases take four chains at a time");
+  extern __shared__ float lds[];
+  float* Xb = lds;                      // [k][chain] xi, then xprop
+  float* Zb = Xb + D * kLd;             // [k][chain] z, then D = xprop - m, then delta
+  float* tsum = Zb + D * kLd;           // [NT][64] potential partials per row tile
+  float* uu = tsum + NT * 64;           // [64]
+  int* flag = (int*)(uu + 64);          // [64]
+  float* alph = (float*)(flag + 64);    // [64]
+  float* msh = alph + 64;               // [D] target mean m
+  const f32x4* LP = (const f32x4*)pack;
+  const f32x4* PP = LP + NPAIR * 256;
+  const int tid = threadIdx.x;
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
+  const float c0p = p.model.data[D + D * D];
+  const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
+  const float el = amh_expf(p.lam[0]);
+  for (int k = tid; k < D; k += 64 * kFBWaves) msh[k] = p.model.data[k];
+  float mu_l[NQ];
+  static_for<NQ>([&](auto Q) { mu_l[Q] = (64 * Q + lane < D) ? p.mu[64 * Q + lane] : 0.0f; });
+  // row tile of this wave in the proposal (both chain halves): at NT = 8 the
+  // waves w and w + 4 that share a SIMD take T and 7 - T (equal MFMA sums)
+  const int pT = (NT == 8) ? ((w < 4) ? 7 - w : w - 4) : ((w < NT) ? w : -1);
+  const int qT = (w < NT) ? w : -1;  // potential row tile (both chain halves)
+  int sI[NS], sJ[NS];
+  static_for<NS>([&](auto S) {
+    const int u = w + kFBWaves * S;
+    int I = 0;
+    while ((I + 1) * (I + 2) / 2 <= u) ++I;
+    sI[S] = (u < NPAIR) ? I : -1;
+    sJ[S] = u - I * (I + 1) / 2;
+  });
+
+  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+    f32x16 sacc[NS];
+    static_for<NS>([&](auto S) { sacc[S] = f32x16{}; });
+    float sd = 0.0f, sa = 0.0f;
+    int cnt = 0;
+#pragma unroll 1
+    for (int half = 0; half < kFB / 64; ++half) {
+      const int64_t c0 = chunk * kFB + 64 * half;
+      const int64_t left = p.C - c0;
+      if (left <= 0) break;
+      const int nv = left < 64 ? (int)left : 64;
+      // lane indices as opaque values: keeps the per-register addresses of
+      // every phase from being hoisted out of the loops (register budget)
+      int lo_ = lane;
+      asm volatile("" : "+v"(lo_));
+      const int h = lo_ >> 5, i = lo_ & 31;
+      // (1) z and the noise xi (arwmh.py:162-165), k-major; wave w takes the
+      // chains w, w + 8, ..; lane = coordinate k mod 64
+      float pe_c = 0.0f;
+      {
+        __syncthreads();  // the previous half's readers of Zb / Xb / uu are done
+#pragma unroll 1
+        for (int n0 = 0; n0 < CPW; n0 += 4) {  // four chains' z loads in flight at a time
+        float zv[4][NQ];
+        static_for<4>([&](auto N) {
+          int64_t ch = c0 + w + kFBWaves * (n0 + N);
+          if (ch >= p.C) ch = p.C - 1;
+          static_for<NQ>([&](auto Q) { zv[N][Q] = (64 * Q + lane < D) ? p.z[ch * D + 64 * Q + lane] : 0.0f; });
+        });
+        static_for<4>([&](auto N) {
+          const int cc = w + kFBWaves * (n0 + N);
+          int64_t ch = c0 + cc;
+          if (ch >= p.C) ch = p.C - 1;
+          const uint32_t kk0 = p.keys[2 * ch], kk1 = p.keys[2 * ch + 1];
+          static_for<NQ>([&](auto Q) {
+            const int k = 64 * Q + lane;
+            if (k < D) {
+#ifndef AMH_FB_NORNG
+              const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)it, 0u, AMH_TAG_STEP, kk0, kk1);
+              Xb[k * kLd + cc] = amh_normal_from_bits(o.v[0]);
+              if (k == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
+#else
+              Xb[k * kLd + cc] = (float)((kk0 + k) & 15) * 0.1f - 0.75f;
+              if (k == 0) uu[cc] = 0.5f;
+#endif
+              Zb[k * kLd + cc] = zv[N][Q];
+            }
+          });
+        });
+        }
+        pe_c = (tid < nv) ? p.pe[c0 + tid] : 0.0f;
+      }
+      __syncthreads();
+      // (2) proposal: acc = L xi over k < 32 (T + 1) (arwmh.py:166-167), both
+      // chain halves from one A tile
+      {
+        float v0[16], v1[16];
+        if (pT >= 0) {
+          const int T = pT;
+          f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+          const f32x4* a = LP + (T * (T + 1) / 2) * 256 + lane;
+          f32x4 cur[4], nxt[4];
+          static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
+          #ifndef AMH_FB_NOPROP
+#pragma unroll 1
+          for (int J = 0; J <= T; ++J) {
+            if (J < T) static_for<4>([&](auto KB) { nxt[KB] = a[256 * (J + 1) + 64 * KB]; });
+            const float* xb = Xb + (32 * J + h) * kLd + i;
+            static_for<4>([&](auto KB) {
+              static_for<4>([&](auto E) {
+                const int ko = 8 * KB + 2 * E;
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], xb[ko * kLd], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], xb[ko * kLd + 32], acc1, 0, 0, 0);
+              });
+            });
+            if (J < T) static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
+          }
+#endif
+          static_for<16>([&](auto R) {
+            const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+            v0[R] = fmaf(el, acc0[(int)R], p.eps * Xb[rr * kLd + i]);
+            v1[R] = fmaf(el, acc1[(int)R], p.eps * Xb[rr * kLd + 32 + i]);
+          });
+        }
+        __syncthreads();
+        // xprop = z + (e^lam L xi + eps xi) -> Xb; D = xprop - m -> Zb
+        if (pT >= 0) {
+          static_for<16>([&](auto R) {
+            const int rr = 32 * pT + (R & 3) + 8 * (R >> 2) + 4 * h;
+            const int o = rr * kLd + i;
+            const float xp0 = Zb[o] + v0[R];
+            const float xp1 = Zb[o + 32] + v1[R];
+            Xb[o] = xp0;
+            Xb[o + 32] = xp1;
+            Zb[o] = xp0 - msh[rr];
+            Zb[o + 32] = xp1 - msh[rr];
+          });
+        }
+      }
+      __syncthreads();
+      // (3) U(xprop) on MFMA: Y = P D, q_r = D_r y_r, tile partials in row order
+      if (qT >= 0) {
+        const int T = qT;
+        f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+        const f32x4* a = PP + (T * NT) * 256 + lane;
+        f32x4 cur[4], nxt[4];
+        static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
+        #ifndef AMH_FB_NOPOT
+#pragma unroll 1
+        for (int J = 0; J < NT; ++J) {
+          if (J + 1 < NT) static_for<4>([&](auto KB) { nxt[KB] = a[256 * (J + 1) + 64 * KB]; });
+          const float* zb = Zb + (32 * J + h) * kLd + i;
+          static_for<4>([&](auto KB) {
+            static_for<4>([&](auto E) {
+              const int ko = 8 * KB + 2 * E;
+              acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], zb[ko * kLd], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], zb[ko * kLd + 32], acc1, 0, 0, 0);
+            });
+          });
+          if (J + 1 < NT) static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
+        }
+#endif
+        float ps0 = 0.0f, ps1 = 0.0f;
+        static_for<16>([&](auto R) {
+          const int row = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+          ps0 = ps0 + Zb[row * kLd + i] * acc0[(int)R];
+          ps1 = ps1 + Zb[row * kLd + 32 + i] * acc1[(int)R];
+        });
+        const float o0 = __shfl_xor(ps0, 32, 64), o1 = __shfl_xor(ps1, 32, 64);
+        const float t0 = (h == 0) ? ps0 + o0 : o0 + ps0;
+        const float t1 = (h == 0) ? ps1 + o1 : o1 + ps1;
+        if (h == 0) {
+          tsum[T * 64 + i] = t0;
+          tsum[T * 64 + 32 + i] = t1;
+        }
+      }
+      __syncthreads();
+      // (4) accept / reject (arwmh.py:173-178)
+      if (tid < 64) {
+        int acc_f = 0;
+        float a = 0.0f;
+        if (tid < nv) {
+          float S = 0.0f;
+          static_for<NT>([&](auto I) { S = S + tsum[I * 64 + tid]; });
+          float pp = (0.5f * S) + c0p;
+          if (amh_isnan(pp)) pp = INFINITY;
+          const float ex = amh_expf(pe_c - pp);
+          a = (ex > 1.0f) ? 1.0f : ex;
+          acc_f = uu[tid] < a;
+          p.pe_out[c0 + tid] = acc_f ? pp : pe_c;
+        }
+        flag[tid] = acc_f;
+        alph[tid] = a;
+      }
+      __syncthreads();
+      // (5) z' out, delta = z' - mu in place of D (k-major; z re-read, L2-hot)
+#pragma unroll 1
+      for (int n0 = 0; n0 < CPW; n0 += 4) {
+        float zr[4][NQ];  // z of the rejected chains, four chains' loads in flight
+        static_for<4>([&](auto N) {
+          const int cc = w + kFBWaves * (n0 + N);
+          const int64_t ch = c0 + cc;
+          const bool ld = cc < nv && flag[cc] == 0;
+          static_for<NQ>([&](auto Q) {
+            const int k = 64 * Q + lane;
+            zr[N][Q] = (ld && k < D) ? p.z[ch * D + k] : 0.0f;
+          });
+        });
+        static_for<4>([&](auto N) {
+          const int cc = w + kFBWaves * (n0 + N);
+          const int64_t ch = c0 + cc;
+          const bool fl = flag[cc] != 0;
+          static_for<NQ>([&](auto Q) {
+            const int k = 64 * Q + lane;
+            if (k < D) {
+              float dv = 0.0f;
+              if (cc < nv) {
+                const float zn = fl ? Xb[k * kLd + cc] : zr[N][Q];
+                p.z_out[ch * D + k] = zn;
+                dv = zn - mu_l[Q];
+              }
+              Zb[k * kLd + cc] = dv;
+            }
+          });
+        });
+      }
+      __syncthreads();
+      // (6) the chunk's sums: S_d, S_a sequential over chains, S_dd on MFMA
+      if (tid < D) {
+        for (int c = 0; c < nv; ++c) sd = sd + Zb[tid * kLd + c];
+      }
+      if (tid == 64 * kFBWaves - 1) {
+        for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+      }
+      cnt += nv;
+#ifndef AMH_FB_NOSDD
+      static_for<NS>([&](auto S) {
+        if (sI[S] >= 0) {
+          const int ra = (32 * sI[S] + i) * kLd, rb = (32 * sJ[S] + i) * kLd;
+          int kk = 0;
+#pragma unroll 1
+          for (; kk + 16 <= nv; kk += 16) {
+            float a[8], b[8];
+            static_for<8>([&](auto Q) {
+              a[Q] = Zb[ra + kk + 2 * Q + h];
+              b[Q] = Zb[rb + kk + 2 * Q + h];
+            });
+            static_for<8>([&](auto Q) { sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], sacc[S], 0, 0, 0); });
+          }
+          for (; kk < nv; kk += 2)
+            sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(Zb[ra + kk + h], Zb[rb + kk + h], sacc[S], 0, 0, 0);
+        }
+      });
+#endif
+    }
+    double* out = p.partials + chunk * V;
+    int lo_ = lane;
+    asm volatile("" : "+v"(lo_));
+    if (tid < D) out[tid] = (double)sd;
+    if (tid == 64 * kFBWaves - 1) {
+      out[V - 2] = (double)sa;
+      out[V - 1] = (double)cnt;
+    }
+    // S_dd tiles in register order: one coalesced 512-B row per register
+    static_for<NS>([&](auto S) {
+      if (sI[S] >= 0) {
+        double* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lo_;
+        static_for<16>([&](auto R) { o[64 * R] = (double)sacc[S][(int)R]; });
+      }
+    });
+  }
 }
 
 // ------------------------------------------------------------------ update --
@@ -744,12 +868,12 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
 
 // --------------------------------------------------------------- launchers --
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
-                         hipStream_t s);
+                         hipStream_t s, int tile_d = 0);
 
 // chains per chunk of the sums (bit spec): 64 at d = 64 (the fused kernel's
 // block), 256 above
 int64_t pooled_big_chunks(int64_t C, int d) {
-  const int64_t ch = (d == kF) ? kFChunk : kBigChunk;
+  const int64_t ch = (d == kF) ? kFChunk : kFB;
   return (C + ch - 1) / ch;
 }
 
@@ -767,27 +891,34 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     if (e != hipSuccess) return e;
     return pooled_reduce(p.partials, nch, V, sums, p.accumulate, s);
   }
-  hipLaunchKernelGGL(pooled_big_propose_kernel, dim3((unsigned)((p.C + 63) / 64)), dim3(256),
-                     (size_t)d * kLd * sizeof(float), s, p, xprop);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  PotParams q{xprop, pep, p.C, d, p.model};
-  e = run_big_potential(q, s);
-  if (e != hipSuccess) return e;
-  const int64_t nch = pooled_big_chunks(p.C, d);
-  // split each chunk's tile pairs over enough blocks to cover the CUs
-  const int nt = d / 32, npairs = nt * (nt + 1) / 2;
-  int split = (int)((256 + nch - 1) / nch);
-  const int max_split = (npairs + 7) / 8;  // at least 8 pairs (one per wave) per part
-  if (split > max_split) split = max_split;
-  if (split < 1) split = 1;
-  const int per = (npairs + split - 1) / split;
-  split = (npairs + per - 1) / per;
-  hipLaunchKernelGGL(pooled_big_stats_kernel, dim3((unsigned)nch, (unsigned)split), dim3(512),
-                     ((size_t)d * kLd + 128) * sizeof(float), s, p, (const float*)xprop, (const float*)pep, per);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return pooled_reduce(p.partials, nch, V, sums, p.accumulate, s);
+  {
+    const int nt = d / 32;
+    const int64_t nch = pooled_big_chunks(p.C, d);
+    float* pack = xprop;  // the caller's scratch: pooled_big_pack_floats(d) floats
+    hipLaunchKernelGGL(pooled_pack_kernel, dim3((unsigned)(nt * (nt + 1) / 2 + nt * nt)), dim3(256), 0, s, p.L,
+                       p.model.data + d, d, pack);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const int64_t grid = nch < (int64_t)cus ? nch : (int64_t)cus;
+    switch (nt) {
+#define AMH_FB(NT_)                                                                                          \
+  case NT_:                                                                                                  \
+    hipLaunchKernelGGL(pooled_fused_big_kernel<NT_>, dim3((unsigned)grid), dim3(64 * kFBWaves), fused_big_lds_bytes<NT_>(), s, \
+                       p, (const float*)pack, nch);                                                          \
+    break;
+      AMH_FB(3) AMH_FB(4) AMH_FB(5) AMH_FB(6) AMH_FB(7) AMH_FB(8)
+#undef AMH_FB
+      default:
+        return hipErrorInvalidValue;
+    }
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    (void)pep;
+    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d);
+  }
 }
 
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {

@@ -507,8 +507,8 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
   const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains, d) : (num_chains + chunk - 1) / chunk;
-  const size_t need = (size_t)amh::pooled_scratch_rows(n_chunks) * (size_t)(d + (int64_t)d * (d + 1) / 2 + 2) *
-                      sizeof(double);
+  const int64_t vrow = (big && d != 64) ? amh::pooled_big_tile_V(d) : d + (int64_t)d * (d + 1) / 2 + 2;
+  const size_t need = (size_t)amh::pooled_scratch_rows(n_chunks) * (size_t)vrow * sizeof(double);
   if (need > h->partials_bytes) {
     if (h->partials) {
       (void)hipStreamSynchronize((hipStream_t)stream);  // a queued launch may still use the old scratch
@@ -537,7 +537,8 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
   p.model = h->model;
   p.k_steps = k_steps;
   if (big) {
-    const size_t nb = (size_t)num_chains * (size_t)(d + 1) * sizeof(float);
+    // xprop + U(xprop) of the unfused path, or the fused path's A-operand copies
+    const size_t nb = ((size_t)num_chains * (size_t)(d + 1) + (size_t)amh::pooled_big_pack_floats(d)) * sizeof(float);
     h->big_ready_C = -1;
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;

@@ -120,6 +120,8 @@ struct PooledUpdateParams {
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);
 // large dimensions (amh_big_pooled.hip): chunks of 256 chains
 int64_t pooled_big_chunks(int64_t C, int d);
+int64_t pooled_big_pack_floats(int d);
+int64_t pooled_big_tile_V(int d);  // partial row length of the fused large-d stats (d > 64)  // scratch floats of the fused large-d stats (A-operand tiles)
 int64_t pooled_scratch_rows(int64_t n_chunks);  // partials + group sums of pooled_reduce
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);

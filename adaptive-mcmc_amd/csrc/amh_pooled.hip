@@ -240,27 +240,47 @@ __global__ __launch_bounds__(256) void pooled_group_kernel(const double* __restr
   gsum[g * V + v] = s;
 }
 
+// Row u of a "tile" partial (pooled_fused_big_kernel, d > 64): [d S_d | NPAIR
+// 32x32 tiles of S_dd in MFMA register order (pair, reg R, lane) | S_a | N]
+// -> its index in the packed sums vector (-1: above the diagonal of a
+// diagonal tile, not part of the sums).
+__device__ int64_t tile_to_packed(int64_t u, int64_t Vt, int d) {
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  if (u < d) return u;
+  if (u >= Vt - 2) return u - Vt + d + P + 2;
+  const int64_t q = u - d;
+  const int pair = (int)(q >> 10), R = (int)((q >> 6) & 15), lane = (int)(q & 63);
+  int I = 0;
+  while ((I + 1) * (I + 2) / 2 <= pair) ++I;
+  const int J = pair - I * (I + 1) / 2;
+  const int row = 32 * I + (R & 3) + 8 * (R >> 2) + 4 * (lane >> 5), col = 32 * J + (lane & 31);
+  if (row < col) return -1;
+  return d + (int64_t)col * d - (int64_t)col * (col - 1) / 2 + (row - col);
+}
+
 __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
-                                                           double* sums, int accumulate) {
-  const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (v >= V) return;
+                                                           double* sums, int accumulate, int tile_d) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= V) return;
+  const int64_t v = tile_d ? tile_to_packed(u, V, tile_d) : u;
+  if (v < 0) return;
   double tot = 0.0;
   int64_t g = 0;
   for (; g + 8 <= n_groups; g += 8) {  // loads in flight, adds in group order
     double x[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = gsum[(g + q) * V + v];
+    for (int q = 0; q < 8; ++q) x[q] = gsum[(g + q) * V + u];
 #pragma unroll
     for (int q = 0; q < 8; ++q) tot += x[q];
   }
-  for (; g < n_groups; ++g) tot += gsum[g * V + v];
+  for (; g < n_groups; ++g) tot += gsum[g * V + u];
   sums[v] = accumulate ? sums[v] + tot : tot;
 }
 
 int64_t pooled_scratch_rows(int64_t n_chunks) { return n_chunks + (n_chunks + kRedGroup - 1) / kRedGroup; }
 
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
-                         hipStream_t s) {
+                         hipStream_t s, int tile_d = 0) {
   const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
   double* gsum = const_cast<double*>(partials) + n_chunks * V;
   const unsigned vb = (unsigned)((V + 255) / 256);
@@ -268,7 +288,7 @@ hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, do
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_final_kernel, dim3(vb), dim3(256), 0, s, (const double*)gsum, n_groups, V, sums,
-                     accumulate);
+                     accumulate, tile_d);
   return hipGetLastError();
 }
 

@@ -1121,8 +1121,9 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
  *            float32 (element (r, k) updated in column order j < k, then
  *            divided by L_kk = sqrtf(A_kk)); as_change per row sequential,
  *            rows by big_sum. */
-/* chains per chunk: 64 at d = 64 (pooled_fused64_kernel), 256 above */
-static int64_t orc_big_chunk(int d) { return d == 64 ? 64 : 256; }
+/* chains per chunk: 64 at d = 64 (pooled_fused64_kernel), 128 above
+ * (pooled_fused_big_kernel: one chunk per block iteration, two 64-chain halves) */
+static int64_t orc_big_chunk(int d) { return d == 64 ? 64 : 128; }
 
 static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
                                  const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
