@@ -616,12 +616,20 @@ __device__ __forceinline__ int a4_base(int d, int j) { return a4_col(d, j) - (j 
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-__global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdateParams p) {
+// 16 waves (115 VGPRs with d a compile-time constant; 8 waves measured
+// 2 % slower at d = 256)
+#ifndef AMH_UPD_WAVES
+#define AMH_UPD_WAVES 16
+#endif
+constexpr int kUpdWaves = AMH_UPD_WAVES;
+
+template <int NT>
+__global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(PooledUpdateParams p) {
   extern __shared__ __attribute__((aligned(16))) float A[];  // A4 layout, float32
-  const int d = p.d;
+  constexpr int d = 32 * NT;  // compile-time: the A4 offsets of every phase fold to constants
   __shared__ int okv;
   __shared__ float rowpart[256];
-  __shared__ __attribute__((aligned(16))) float Lt[32 * 32];  // diagonal block, by column
+  __shared__ __attribute__((aligned(16))) float colbuf[kUpdWaves * 128];  // per-wave column broadcasts
   const int tid = threadIdx.x;
   US_INIT
   const int lane = lane_id();
@@ -644,83 +652,105 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
     const int nA = d * (d + 4) / 2;
     const f32x4* src = (const f32x4*)p.scratch;
     f32x4* dst = (f32x4*)A;
-    for (int q = tid; q < nA / 4; q += 1024) dst[q] = src[q];
+    for (int q = tid; q < nA / 4; q += 64 * kUpdWaves) dst[q] = src[q];
   }
   if (tid == 0) okv = 1;
   __syncthreads();
   US(0)
+#pragma unroll 1
   for (int p0 = 0; p0 < d; p0 += 32) {
-    // (1) diagonal block: wave 0, lane ii (and ii + 32, a duplicate) holds row
-    // p0 + ii.  Column k of the block's factor goes to Lt (dense, Lt[k][m] =
-    // L_{p0+m, p0+k}) and is read back as 16-B broadcasts.  No lane masks: the
-    // entries above the diagonal (m > ii) are updated too and never used, so
-    // nothing row-dependent stays live across the 32 steps.
-    if (w == 0) {
-      const int ii = lane & 31;
-      const int r = p0 + ii;
-      float a[32];
-      static_for<32>([&](auto K) { a[K] = (K <= ii) ? A[a4_base(d, p0 + K) + r] : 0.0f; });
-      bool ok = true;
-      // the next pivot is formed from lane k+1's own two values (readlane),
-      // the same fmaf its rank-one update applies, so the pivot chain does
-      // not wait for the LDS round trip of the column
-      float piv = rdlane(a[0], 0);
-      static_for<32>([&](auto K) {
-        constexpr int k = K;
-        ok = ok && (piv > 0.0f) && amh_isfinite(piv);
-        const float ljj = sqrtf(piv);
-        a[k] = a[k] / ljj;
-        float l1 = 0.0f;  // L_{k+1,k}: column k+1's update and the next pivot skip the LDS round trip
-        if constexpr (k + 1 < 32) {
-          l1 = rdlane(a[k], k + 1);
-          piv = fmaf(-l1, l1, rdlane(a[k + 1], k + 1));
-          a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
-        }
-        Lt[k * 32 + ii] = a[k];
-        Lt[k * 32 + k] = ljj;  // uniform store, after the lane stores
-        if constexpr (k + 1 < 32) {
-          static_for<(32 - ((k + 1) & ~3)) / 4>([&](auto Q) {
-            constexpr int m0 = ((k + 1) & ~3) + 4 * Q;
-            const f32x4 v = *(const f32x4*)&Lt[k * 32 + m0];
-            static_for<4>([&](auto E) {
-              constexpr int m = m0 + E;
-              if constexpr (m > k + 1) a[m] = fmaf(-a[k], v[(int)E], a[m]);
+    // (1) the panel's 32 columns, rows p0 .. d-1, in registers: wave v holds
+    // the diagonal block's rows p0 + ii in lanes ii < 32 (every wave a copy,
+    // so no wave waits for another) and the rows p0 + 32 (v + 1) + ii below
+    // it in lanes 32 + ii.  Column k: pivot from lane k, L_kk = sqrtf, the
+    // whole column divided, then column k's update of the panel's later
+    // columns with L_mk broadcast from lane m (v_readlane) -- per element the
+    // oracle's fmaf chain in column order.  Lanes above the diagonal compute
+    // values that are never used.
+    {
+      const int nbelow = (d - p0 - 32) / 32;  // 32-row blocks below the diagonal block
+      const int nwv = nbelow > 0 ? nbelow : 1;
+      if (w < nwv) {
+        int ln = lane;  // opaque: keeps the per-column lane tests from being hoisted into SGPR spills
+        asm volatile("" : "+v"(ln));
+        const int ii = ln & 31;
+        const bool below = ln >= 32;
+        const bool live = !below || w < nbelow;
+        const int r = below ? (live ? p0 + 32 * (w + 1) + ii : d - 1) : p0 + ii;
+        // unconditional loads: entries above the diagonal read in-range
+        // neighbours (never used), rows past d read row d - 1
+        float a[32];
+        const int ab0 = a4_base(d, p0) + r;
+        static_for<32>([&](auto K) { a[K] = A[ab0 + (a4_base(d, p0 + K) - a4_base(d, p0))]; });
+        US(2)
+        bool ok = true;
+        float* cb = colbuf + 128 * w;  // this wave's column broadcast buffers (two, alternating)
+        // Software pipeline over the columns: column k's pivot, square root
+        // and division come first; then column k-1's LDS-broadcast updates
+        // (m >= k+1, read while column k was being formed) are applied; then
+        // column k goes to LDS and its next-column update a[k+1] is done with
+        // v_readlane.  Every element still sees its updates in column order.
+#ifdef AMH_STAMPS_TWICE
+#pragma unroll 1
+        for (int rep_ = 0; rep_ < 2; ++rep_) {  // diagnostic: second pass with a warm instruction cache
+        if (rep_ == 1) US(5)
+#endif
+        f32x4 pv[8];  // column k-1's broadcast values (rows 4q .. 4q+3)
+        float am1 = 0.0f;
+#ifndef AMH_UPD_NOCOLS
+        static_for<32>([&](auto K) {
+          constexpr int k = K;
+          const float piv = rdlane(a[k], k);
+          ok = ok && (piv > 0.0f) && amh_isfinite(piv);
+          const float ljj = sqrtf(piv);
+          const float q = a[k] / ljj;
+          __builtin_amdgcn_sched_barrier(0);
+          if constexpr (k >= 1) {  // column k-1's updates of rows m >= k+1
+            static_for<8>([&](auto Q) {
+              static_for<4>([&](auto E) {
+                constexpr int m = 4 * Q + E;
+                if constexpr (m >= k + 1) a[m] = fmaf(-am1, pv[(int)Q][(int)E], a[m]);
+              });
             });
+          }
+          a[k] = (ln == k) ? ljj : q;
+          if constexpr (k + 1 < 32) {
+            float* cbk = cb + 64 * (k & 1);
+            cbk[ln] = a[k];
+            static_for<8>([&](auto Q) {
+              if constexpr (4 * Q + 3 >= k + 2) pv[(int)Q] = *(const f32x4*)&cbk[4 * Q];
+            });
+            am1 = a[k];
+            const float l1 = rdlane(a[k], k + 1);
+            a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        });
+#endif
+#ifdef AMH_STAMPS_TWICE
+        }
+#endif
+        US(1)
+        if (w == 0 && lane == 0 && !ok) okv = 0;
+        // branch-free write-back: lanes with nothing to write (above the
+        // diagonal, past d, or a diagonal copy of a wave other than 0) store
+        // to this wave's scratch slot instead
+        {
+          const int dummy = (int)(colbuf + 128 * w + 64 + ln - A);
+          // last column this lane writes: all 32 below the block, K <= ii in
+          // wave 0's copy of the block, none otherwise
+          const int kmax = below ? (live ? 31 : -1) : (w == 0 ? ii : -1);
+          static_for<32>([&](auto K) {
+            const int o = ((int)K <= kmax) ? ab0 + (a4_base(d, p0 + K) - a4_base(d, p0)) : dummy;
+            A[o] = a[K];
           });
         }
-      });
-      if (lane == 0 && !ok) okv = 0;
-      for (int k = 0; k < 32; ++k) {
-        if (lane < 32 && lane >= k) A[a4_base(d, p0 + k) + p0 + lane] = Lt[k * 32 + lane];
       }
     }
-    __syncthreads();
-    US(1)
-    // (2) panel below the block: one thread per row, L_mk of the block as
-    // 16-B broadcasts from Lt
-    const int q0 = p0 + 32;
-    if (tid < d - q0) {
-      const int r = q0 + tid;
-      float a[32];
-      static_for<32>([&](auto K) { a[K] = A[a4_base(d, p0 + K) + r]; });
-      static_for<32>([&](auto K) {
-        constexpr int k = K;
-        const float lrk = a[k] / Lt[k * 32 + k];
-        a[k] = lrk;
-        static_for<(32 - ((k + 1) & ~3)) / 4>([&](auto Q) {
-          constexpr int m0 = ((k + 1) & ~3) + 4 * Q;
-          const f32x4 v = *(const f32x4*)&Lt[k * 32 + m0];
-          static_for<4>([&](auto E) {
-            constexpr int m = m0 + E;
-            if constexpr (m > k) a[m] = fmaf(-lrk, v[(int)E], a[m]);
-          });
-        });
-        asm volatile("" ::: "memory");  // keep the next column's reads after this one's FMAs
-      });
-      static_for<32>([&](auto K) { A[a4_base(d, p0 + K) + r] = a[K]; });
-    }
+    US(7)
     __syncthreads();
     US(2)
+    const int q0 = p0 + 32;
     // (3) trailing update with the panel's 32 columns on MFMA: each wave
     // takes 32x32 tile pairs (I >= J) of the trailing matrix, acc = A_IJ and
     // 16 v_mfma_f32_32x32x2_f32 with A = -L_I (rows x panel columns) and
@@ -730,7 +760,7 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
       const int mt = (d - q0) / 32;
       const int npair = mt * (mt + 1) / 2;
       const int hh = lane >> 5, ii = lane & 31;
-      for (int pp = w; pp < npair; pp += 16) {
+      for (int pp = w; pp < npair; pp += kUpdWaves) {
         int I = 0;
         while ((I + 1) * (I + 2) / 2 <= pp) ++I;
         const int J = pp - I * (I + 1) / 2;
@@ -768,37 +798,53 @@ __global__ __launch_bounds__(1024) void pooled_big_update_kernel(PooledUpdatePar
     const int nA = d * (d + 4) / 2;
     f32x4* dst = (f32x4*)p.scratch;
     const f32x4* src = (const f32x4*)A;
-    for (int q = tid; q < nA / 4; q += 1024) dst[q] = src[q];
+    for (int q = tid; q < nA / 4; q += 64 * kUpdWaves) dst[q] = src[q];
     if (tid == 0) {
       ((int*)p.scratch)[nA] = ok ? 1 : 0;
       p.scratch[nA + 1] = gamma;
     }
   }
   __syncthreads();
-  for (int j = w; j < d; j += 16) {
-    const int64_t co = col_off(d, j);
-    const int len = d - j, ab = a4_base(d, j);
-    float lo[4];
-    static_for<4>([&](auto Q) {
-      const int rr = 64 * Q + lane;
-      lo[Q] = rr < len ? p.in.scale[co + rr] : 0.0f;
+  // four columns' old-factor loads in flight at a time
+  constexpr int NQ = (d + 63) / 64;
+#pragma unroll 1
+  for (int j0 = w; j0 < d; j0 += 4 * kUpdWaves) {
+    float lo[4][NQ];
+    static_for<4>([&](auto U) {
+      const int j = j0 + kUpdWaves * U;
+      const int64_t co = col_off(d, j);
+      static_for<NQ>([&](auto Q) {
+        const int rr = 64 * Q + lane;
+        lo[U][Q] = (j < d && rr < d - j) ? p.in.scale[co + rr] : 0.0f;
+      });
     });
-    static_for<4>([&](auto Q) {
-      const int rr = 64 * Q + lane;
-      if (rr < len) {
-        const float ln = ok ? A[ab + j + rr] : lo[Q];
-        A[ab + j + rr] = (ln * e1) - (lo[Q] * e0);
-      }
+    static_for<4>([&](auto U) {
+      const int j = j0 + kUpdWaves * U;
+      const int ab = a4_base(d, j);
+      static_for<NQ>([&](auto Q) {
+        const int rr = 64 * Q + lane;
+        if (j < d && rr < d - j) {
+          const float ln = ok ? A[ab + j + rr] : lo[U][Q];
+          A[ab + j + rr] = (ln * e1) - (lo[U][Q] * e0);
+        }
+      });
     });
   }
   __syncthreads();
   US(4)
   if (tid < d) {
+    // row r's terms in column order; eight LDS reads in flight (a zero term
+    // past the diagonal adds nothing: s >= +0)
     const int r = tid;
     float s = 0.0f;
-    for (int j = 0; j <= r; ++j) {
-      const float tt = A[a4_base(d, j) + r];
-      s = fmaf(tt, tt, s);
+#pragma unroll 1
+    for (int j0 = 0; j0 <= r; j0 += 8) {
+      float t[8];
+      static_for<8>([&](auto U) {
+        const int j = j0 + U;
+        t[U] = (j <= r) ? A[a4_base(d, j) + r] : 0.0f;
+      });
+      static_for<8>([&](auto U) { s = fmaf(t[U], t[U], s); });
     }
     rowpart[r] = s;
   }
@@ -926,7 +972,16 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
   hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pooled_big_update_kernel, dim3(1), dim3(1024), shm, s, p);
+  switch (p.d / 32) {
+#define AMH_UPD(NT_)                                                                                    \
+  case NT_:                                                                                            \
+    hipLaunchKernelGGL(pooled_big_update_kernel<NT_>, dim3(1), dim3(64 * kUpdWaves), shm, s, p);       \
+    break;
+    AMH_UPD(2) AMH_UPD(3) AMH_UPD(4) AMH_UPD(5) AMH_UPD(6) AMH_UPD(7) AMH_UPD(8)
+#undef AMH_UPD
+    default:
+      return hipErrorInvalidValue;
+  }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_big_post_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);

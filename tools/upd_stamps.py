@@ -34,8 +34,9 @@ buf = np.zeros(8, np.uint64)
 L = _lib.lib()
 L.amh_diag_upd_stamps.argtypes = [ctypes.c_void_p]
 assert L.amh_diag_upd_stamps(buf.ctypes.data) == 0
-names = ["init", "diag blocks", "panel solves", "trailing", "write-out", "as_change rows", "final", "-"]
-tot = buf[:7].sum()
-for n, v in zip(names[:7], buf[:7]):
+names = ["init", "panel columns", "panel loads + barrier", "trailing", "write-out", "as_change rows", "final",
+         "panel write-back"]
+tot = buf[:8].sum()
+for n, v in zip(names, buf[:8]):
     print(f"{n:15s} {int(v):9d} ticks  {100.0 * v / tot:5.1f} %")
 print(f"total {int(tot)} ticks (s_memtime = shader clock; ~{tot / 2400.0:.1f} us at 2.4 GHz)")
