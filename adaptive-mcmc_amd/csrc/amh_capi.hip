@@ -29,6 +29,7 @@ struct amh_handle {
   size_t split_bytes = 0;
   float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
   size_t upd_bytes = 0;
+  float* xpack = nullptr;      // diamonds: design matrix in MFMA tile order (made by amh_bind_model)
   std::string err;
 };
 
@@ -148,6 +149,7 @@ int amh_destroy(amh_handle* h) {
     if (h->partials) (void)hipFree(h->partials);
     if (h->split_buf) (void)hipFree(h->split_buf);
     if (h->upd_buf) (void)hipFree(h->upd_buf);
+    if (h->xpack) (void)hipFree(h->xpack);
   }
   delete h;
   return AMH_OK;
@@ -171,6 +173,22 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
   h->model.n = (model_id == AMH_MODEL_KIDIQ || dia) ? iparams[0] : 0;
   h->model.k = dia ? iparams[1] : 0;
   h->n_data = n_data;
+  if (h->xpack) {
+    (void)hipDeviceSynchronize();  // a queued launch may still read the old copy
+    (void)hipFree(h->xpack);
+    h->xpack = nullptr;
+  }
+  if (model_id == AMH_MODEL_DIAMONDS && amh::split_model(model_id, dm)) {
+    // the MFMA potential's tile copy of Xc and Y, made once here (synchronous)
+    const int64_t nf = amh::diamonds_pack_floats(h->model.n, h->model.k);
+    if (nf > 0) {
+      hipError_t e = hipSetDevice(h->device);
+      if (e == hipSuccess) e = hipMalloc(&h->xpack, (size_t)nf * sizeof(float));
+      if (e == hipSuccess) e = amh::run_diamonds_pack(h->model, h->xpack, nullptr);
+      if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_bind_model(diamonds tile copy)");
+    }
+  }
   return AMH_OK;
 }
 
@@ -201,7 +219,7 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
     // pe0 = U(z0) from the lane-per-chain potential (bit-identical to the group one)
     e = amh::run_init_nopot(p, (hipStream_t)stream);
     if (e == hipSuccess) {
-      amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model};
+      amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model, h->xpack};
       e = amh::run_potential_lane(h->model_id, q, (hipStream_t)stream);
     }
   } else {
@@ -318,7 +336,7 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
       q.col_pe = (keep && p.col_pe) ? p.col_pe + (size_t)k * C : nullptr;
       e = amh::run_propose(q, xprop, (hipStream_t)stream);
       if (e == hipSuccess) {
-        amh::PotParams pp{xprop, peprop, C, p.d, h->model};
+        amh::PotParams pp{xprop, peprop, C, p.d, h->model, h->xpack};
         e = amh::run_potential_lane(h->model_id, pp, (hipStream_t)stream);
       }
       if (e == hipSuccess) e = amh::run_step_ext(q, (hipStream_t)stream);
@@ -337,7 +355,7 @@ int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* str
   if (!z || !pe || n < 1) return fail(h, AMH_EINVAL, "amh_potential: bad arguments");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential/hipSetDevice");
-  amh::PotParams p{z, pe, n, h->cfg.dim, h->model};
+  amh::PotParams p{z, pe, n, h->cfg.dim, h->model, h->xpack};
   e = amh::big_model(h->model_id, p.d)     ? amh::run_big_potential(p, (hipStream_t)stream)
       : amh::split_model(h->model_id, p.d) ? amh::run_potential_lane(h->model_id, p, (hipStream_t)stream)
                                            : amh::run_potential(h->model_id, p, (hipStream_t)stream);

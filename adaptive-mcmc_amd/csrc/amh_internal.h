@@ -50,6 +50,7 @@ struct PotParams {
   int64_t n;
   int32_t d;
   ModelArgs model;
+  const float* xpack = nullptr;  // diamonds: the design matrix in MFMA tile order (diamonds_pack_kernel)
 };
 
 struct PnxParams {
@@ -167,6 +168,9 @@ hipError_t run_big_potential(const PotParams& p, hipStream_t s);
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain
 // batched potential, then the step kernel reading U(z') (amh_split.hip)
 bool split_model(int model_id, int d);
+constexpr int kDiaMfmaKc = 24;  // diamonds on MFMA: the reference data set's Kc (amh_split.hip)
+int64_t diamonds_pack_floats(int64_t N, int64_t K);  // 0: no MFMA path for this shape
+hipError_t run_diamonds_pack(const ModelArgs& m, float* xp, hipStream_t s);
 // the reference diamonds data (K = 25 columns): d = 26, compiled as a fixed
 // dimension on the split path
 constexpr int kDiamondsD = 26;

@@ -221,6 +221,160 @@ __global__ __launch_bounds__(64 * kDiaWaves) void diamonds_pot_lane_kernel(PotPa
   if (c < n_ch) p.pe[c] = -(((ll + lpb) + lpi) + lps);
 }
 
+// --------------------------------------------------- diamonds on MFMA --
+// mu = Xc b for 32 rows x 32 chains per v_mfma_f32_32x32x2_f32 accumulation
+// (A = a 32-row tile of Xc, B = the chains' coefficients; KC/2 MFMAs over k
+// in order from 0 -- per element the fmaf chain of the bit spec, so the bits
+// equal the lane kernel's).  Accumulator register R of lane (i, h) holds row
+// 32 m + (R&3) + 8 (R>>2) + 4 h of chain i: the residue of the bit spec's 32
+// partial sums is fixed per register, and the tiles arrive in row order, so
+// part[R] = fmaf(e, e, part[R]) keeps every residue's row order.  Xc and Y
+// are read from a per-model tile copy in A-operand / register order
+// (diamonds_pack_kernel, made when the model is bound).  A wave serves 64
+// chains (two B tiles sharing each A tile); rows past N add nothing.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+template <int KC>
+struct DiaMfma {
+  static constexpr int S = (KC + 1) / 2;   // MFMA k steps per tile
+  static constexpr int G = (S + 3) / 4;    // 16-B A vectors per lane per tile
+  static constexpr int64_t tiles(int64_t N) { return (N + 31) / 32; }
+  static constexpr int64_t floats(int64_t N) { return tiles(N) * (G * 256 + 32); }
+};
+
+template <int KC>
+__global__ __launch_bounds__(256) void diamonds_pack_kernel(const float* __restrict__ data, int64_t N,
+                                                            float* __restrict__ xp) {
+  using T = DiaMfma<KC>;
+  const int64_t m = blockIdx.x;
+  const int t = threadIdx.x;
+  const float* X = data;
+  const float* Y = data + N * KC;
+  if (t < T::G * 64) {
+    const int g = t >> 6, lane = t & 63, i = lane & 31, h = lane >> 5;
+    const int64_t row = 32 * m + i;
+    f32x4 v;
+    static_for<4>([&](auto E) {
+      const int k = 2 * (4 * g + E) + h;
+      v[(int)E] = (row < N && k < KC) ? X[row * KC + k] : 0.0f;
+    });
+    ((f32x4*)xp)[(m * T::G + g) * 64 + lane] = v;
+  } else if (t < T::G * 64 + 32) {
+    const int q = t - T::G * 64, h = q >> 4, R = q & 15;
+    const int64_t row = 32 * m + (R & 3) + 8 * (R >> 2) + 4 * h;
+    xp[T::tiles(N) * T::G * 256 + 32 * m + q] = row < N ? Y[row] : 0.0f;
+  }
+}
+
+template <int KC>
+__global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) {
+  using T = DiaMfma<KC>;
+  constexpr int S = T::S, G = T::G;
+  const int d = p.d;
+  const int64_t N = p.model.n;
+  const int64_t NT = T::tiles(N);
+  const int64_t n_ch = p.n;
+  const int lane = lane_id();
+  const int i = lane & 31, h = lane >> 5;
+  const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  const int64_t cb = ((int64_t)blockIdx.x * 4 + w) * 64;
+  const int64_t c0 = cb + i, c1 = cb + 32 + i;
+  const float* z0 = p.z + (c0 < n_ch ? c0 : n_ch - 1) * d;
+  const float* z1 = p.z + (c1 < n_ch ? c1 : n_ch - 1) * d;
+  float B0[S], B1[S];
+  static_for<S>([&](auto Q) {
+    const int k = 2 * Q + h;
+    B0[Q] = k < KC ? z0[1 + k] : 0.0f;
+    B1[Q] = k < KC ? z1[1 + k] : 0.0f;
+  });
+  const float icpt0 = z0[0], icpt1 = z1[0];
+  const float isg0 = 1.0f / amh_expf(z0[KC + 1]), isg1 = 1.0f / amh_expf(z1[KC + 1]);
+  const f32x4* xa = (const f32x4*)p.xpack + lane;
+  const f32x4* ya = (const f32x4*)(p.xpack + NT * G * 256) + 4 * h;
+  float part0[16], part1[16];
+  static_for<16>([&](auto R) {
+    part0[R] = 0.0f;
+    part1[R] = 0.0f;
+  });
+  f32x4 a[G], y[4];
+  static_for<G>([&](auto Q) { a[Q] = xa[64 * Q]; });
+  static_for<4>([&](auto Q) { y[Q] = ya[Q]; });
+#pragma unroll 1
+  for (int64_t m = 0; m < NT; ++m) {
+    f32x4 an[G], yn[4];
+    const int64_t mn = (m + 1 < NT) ? m + 1 : m;  // next tile's loads in flight during this one
+    static_for<G>([&](auto Q) { an[Q] = xa[(mn * G + Q) * 64]; });
+    static_for<4>([&](auto Q) { yn[Q] = ya[8 * mn + Q]; });
+    f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+    static_for<S>([&](auto Q) {
+      const float av = a[Q / 4][Q % 4];
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B0[Q], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B1[Q], acc1, 0, 0, 0);
+    });
+    const int64_t nrem = N - 32 * m;  // rows of this tile that exist
+    static_for<16>([&](auto R) {
+      const int rr = (R & 3) + 8 * (R >> 2) + 4 * h;
+      const float yv = y[R / 4][R % 4];
+      const float e0 = (yv - (icpt0 + acc0[(int)R])) * isg0;
+      const float e1 = (yv - (icpt1 + acc1[(int)R])) * isg1;
+      const bool ok = rr < nrem;
+      part0[R] = ok ? fmaf(e0, e0, part0[R]) : part0[R];
+      part1[R] = ok ? fmaf(e1, e1, part1[R]) : part1[R];
+    });
+    static_for<G>([&](auto Q) { a[Q] = an[Q]; });
+    static_for<4>([&](auto Q) { y[Q] = yn[Q]; });
+  }
+  // lane (i, 0) finishes chain c0, lane (i, 1) chain c1: the other half's
+  // residues arrive by a 32-lane swap
+  float all[32];
+  static_for<16>([&](auto R) {
+    const float mine = h ? part1[R] : part0[R];
+    const float other = __shfl_xor(h ? part0[R] : part1[R], 32, 64);
+    const int rm = (R & 3) + 8 * (R >> 2);
+    if (h == 0) {
+      all[rm] = mine;
+      all[rm + 4] = other;
+    } else {
+      all[rm + 4] = mine;
+      all[rm] = other;
+    }
+  });
+  const float Ssum = butterfly32(all);
+  const int64_t c = h ? c1 : c0;
+  const float* zc = h ? z1 : z0;
+  float bb[32];
+  static_for<32>([&](auto R) {
+    constexpr int r = R;
+    if constexpr (r >= 1 && r <= KC) {
+      const float br = zc[r];
+      bb[r] = br * br;
+    } else {
+      bb[r] = 0.0f;
+    }
+  });
+  const float Bsum = butterfly32(bb);
+  const float icpt = zc[0];
+  const float ls = zc[KC + 1];
+  const float sg = amh_expf(ls);
+  const float cst = -3.30347394261755545f;
+  const float ll = fmaf(-0.5f, Ssum, (float)N * ((-ls) - HALF_LOG_2PI));
+  const float lpb = fmaf(-0.5f, Bsum, -(float)KC * HALF_LOG_2PI);
+  const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+  const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+  if (c < n_ch) p.pe[c] = -(((ll + lpb) + lpi) + lps);
+}
+
+int64_t diamonds_pack_floats(int64_t N, int64_t K) {
+  return (K - 1 == kDiaMfmaKc) ? DiaMfma<kDiaMfmaKc>::floats(N) : 0;
+}
+
+hipError_t run_diamonds_pack(const ModelArgs& m, float* xp, hipStream_t s) {
+  if (m.k - 1 != kDiaMfmaKc || m.n < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(diamonds_pack_kernel<kDiaMfmaKc>, dim3((unsigned)DiaMfma<kDiaMfmaKc>::tiles(m.n)), dim3(256), 0,
+                     s, m.data, m.n, xp);
+  return hipGetLastError();
+}
+
 // ---------------------------------------------------------------- launchers --
 hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
   if (p.d < 1 || p.d > 32) return hipErrorInvalidValue;
@@ -238,6 +392,10 @@ hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
 
 hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s) {
   if (!split_model(model_id, p.d)) return hipErrorInvalidValue;
+  if (p.xpack != nullptr && p.model.k - 1 == kDiaMfmaKc && p.d == kDiaMfmaKc + 2) {
+    hipLaunchKernelGGL(diamonds_pot_mfma_kernel<kDiaMfmaKc>, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
+    return hipGetLastError();
+  }
   const int64_t blocks = (p.n + 127) / 128;
   if (p.model.k - 1 == 24) {
     hipLaunchKernelGGL(diamonds_pot_lane_kernel<24>, dim3((unsigned)blocks), dim3(64 * kDiaWaves), 0, s, p);
