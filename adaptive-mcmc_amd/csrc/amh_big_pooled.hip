@@ -366,17 +366,37 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
       {
         __syncthreads();  // the previous half's readers of Zb / Xb / uu are done
 #pragma unroll 1
-        for (int n0 = 0; n0 < CPW; n0 += 4) {  // four chains' z loads in flight at a time
-        float zv[4][NQ];
+        for (int n0 = 0; n0 < CPW; n0 += 4) {  // four chains' z (and noise) loads in flight at a time
+        float zv[4][NQ], xv[4][NQ];
+        bool use[4];
+        uint32_t ub[4];
         static_for<4>([&](auto N) {
           int64_t ch = c0 + w + kFBWaves * (n0 + N);
           if (ch >= p.C) ch = p.C - 1;
+          use[N] = false;
+          ub[N] = 0u;
+          if (p.xi != nullptr && ch < p.xi_cap) {  // noise drawn ahead: only if its record is this draw's
+            const uint4 rec = p.xrec[ch];
+            use[N] = rec.x == (uint32_t)it && rec.y == p.keys[2 * ch] && rec.z == p.keys[2 * ch + 1];
+            ub[N] = rec.w;
+          }
           static_for<NQ>([&](auto Q) { zv[N][Q] = (64 * Q + lane < D) ? p.z[ch * D + 64 * Q + lane] : 0.0f; });
+          if (use[N]) static_for<NQ>([&](auto Q) { xv[N][Q] = (64 * Q + lane < D) ? p.xi[ch * D + 64 * Q + lane] : 0.0f; });
         });
         static_for<4>([&](auto N) {
           const int cc = w + kFBWaves * (n0 + N);
           int64_t ch = c0 + cc;
           if (ch >= p.C) ch = p.C - 1;
+          if (use[N]) {
+            static_for<NQ>([&](auto Q) {
+              const int k = 64 * Q + lane;
+              if (k < D) {
+                Xb[k * kLd + cc] = xv[N][Q];
+                if (k == 0) uu[cc] = amh_unif01_from_bits(ub[N]);
+                Zb[k * kLd + cc] = zv[N][Q];
+              }
+            });
+          } else {
           const uint32_t kk0 = p.keys[2 * ch], kk1 = p.keys[2 * ch + 1];
           static_for<NQ>([&](auto Q) {
             const int k = 64 * Q + lane;
@@ -392,6 +412,7 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
               Zb[k * kLd + cc] = zv[N][Q];
             }
           });
+          }
         });
         }
         pe_c = (tid < nv) ? p.pe[c0 + tid] : 0.0f;
@@ -559,19 +580,20 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
       });
 #endif
     }
-    double* out = p.partials + chunk * V;
+    // float32 partials (pooled_group_kernel<float> widens them exactly)
+    float* out = (float*)p.partials + chunk * V;
     int lo_ = lane;
     asm volatile("" : "+v"(lo_));
-    if (tid < D) out[tid] = (double)sd;
+    if (tid < D) out[tid] = sd;
     if (tid == 64 * kFBWaves - 1) {
-      out[V - 2] = (double)sa;
-      out[V - 1] = (double)cnt;
+      out[V - 2] = sa;
+      out[V - 1] = (float)cnt;
     }
-    // S_dd tiles in register order: one coalesced 512-B row per register
+    // S_dd tiles in register order: one coalesced 256-B row per register
     static_for<NS>([&](auto S) {
       if (sI[S] >= 0) {
-        double* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lo_;
-        static_for<16>([&](auto R) { o[64 * R] = (double)sacc[S][(int)R]; });
+        float* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lo_;
+        static_for<16>([&](auto R) { o[64 * R] = sacc[S][(int)R]; });
       }
     });
   }
@@ -623,12 +645,63 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 #endif
 constexpr int kUpdWaves = AMH_UPD_WAVES;
 
+// Trailing update of one 32x32 tile (I >= J, in 32-row blocks of the
+// trailing matrix that starts at row / column q0) by the panel of columns
+// p0 .. p0 + 31 on MFMA: acc = A_IJ and 16 v_mfma_f32_32x32x2_f32 with
+// A = -L_I (rows x panel columns) and B = L_J^T -- per element the fmaf chain
+// fmaf(-L_rj, L_cj, .) over j = p0 .. p0 + 31 in order, the oracle's bits.
+__device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, int I, int J, int lane) {
+  const int hh = lane >> 5, ii = lane & 31;
+  const int rI = q0 + 32 * I, cJ = q0 + 32 * J;
+  f32x16 acc;
+  const int col = cJ + ii;
+  const int cb = a4_base(d, col);
+  static_for<16>([&](auto R) {
+    const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
+    acc[(int)R] = (row >= (col & ~3)) ? A[cb + row] : 0.0f;
+  });
+  static_for<16>([&](auto K2) {
+    const int k = p0 + 2 * K2 + hh;
+    const int kb = a4_base(d, k);
+    const float av = -A[kb + rI + ii];
+    const float bv = A[kb + cJ + ii];
+    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  });
+  static_for<16>([&](auto R) {
+    const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
+    if (row >= col) A[cb + row] = acc[(int)R];
+  });
+}
+
 template <int NT>
 __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(PooledUpdateParams p) {
   extern __shared__ __attribute__((aligned(16))) float A[];  // A4 layout, float32
   constexpr int d = 32 * NT;  // compile-time: the A4 offsets of every phase fold to constants
+  if (blockIdx.x > 0) {
+    // extra blocks (one per CU, beside the single-workgroup factorisation):
+    // the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
+    // Philox(0, i', 0)[1] of every chain, i' = i + K (pooled_big_prep_kernel
+    // left it in the staging buffer), each chain's row with its record
+    const int32_t inext = ((const int*)p.scratch)[d * (d + 4) / 2 + 4];
+    const int lane = lane_id();
+    const int64_t wv = (int64_t)(blockIdx.x - 1) * kUpdWaves + threadIdx.x / 64;
+    const int64_t nw = (int64_t)(gridDim.x - 1) * kUpdWaves;
+    for (int64_t ch = wv; ch < p.noise_C; ch += nw) {
+      const uint32_t kk0 = p.keys[2 * ch], kk1 = p.keys[2 * ch + 1];
+      uint32_t ubits = 0u;
+      static_for<(d + 63) / 64>([&](auto Q) {
+        const int k = 64 * Q + lane;
+        if (k < d) {
+          const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0, kk1);
+          p.xi[ch * d + k] = amh_normal_from_bits(o.v[0]);
+          if (k == 0) ubits = o.v[1];
+        }
+      });
+      if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0, kk1, ubits);
+    }
+    return;
+  }
   __shared__ int okv;
-  __shared__ float rowpart[256];
   __shared__ __attribute__((aligned(16))) float colbuf[kUpdWaves * 128];  // per-wave column broadcasts
   const int tid = threadIdx.x;
   US_INIT
@@ -748,52 +821,36 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
       }
     }
     US(7)
-    __syncthreads();
-    US(2)
-    const int q0 = p0 + 32;
-    // (3) trailing update with the panel's 32 columns on MFMA: each wave
-    // takes 32x32 tile pairs (I >= J) of the trailing matrix, acc = A_IJ and
-    // 16 v_mfma_f32_32x32x2_f32 with A = -L_I (rows x panel columns) and
-    // B = L_J^T -- per element the fmaf chain fmaf(-L_rj, L_cj, .) over
-    // j = 0..31 in order, the bits of the VALU form it replaces.
-    {
+    // (2) look-ahead: while the panel's columns are factored, the other waves
+    // apply the previous panel's trailing update to the column blocks right
+    // of this panel (that panel's tiles with J >= 1; its J = 0 column block
+    // -- this panel -- was updated before this panel was loaded)
+    if (p0 >= 32) {
+      const int nbelow = (d - p0 - 32) / 32;
+      const int nwv = nbelow > 0 ? nbelow : 1;
+      const int q0 = p0;  // first row / column of the previous panel's trailing matrix
       const int mt = (d - q0) / 32;
-      const int npair = mt * (mt + 1) / 2;
-      const int hh = lane >> 5, ii = lane & 31;
-      for (int pp = w; pp < npair; pp += kUpdWaves) {
+      const int npair1 = mt * (mt - 1) / 2;  // tile pairs with J >= 1
+      for (int u = w - nwv; u >= 0 && u < npair1; u += kUpdWaves - nwv) {
         int I = 0;
-        while ((I + 1) * (I + 2) / 2 <= pp) ++I;
-        const int J = pp - I * (I + 1) / 2;
-        const int rI = q0 + 32 * I, cJ = q0 + 32 * J;
-        f32x16 acc;
-        const int col = cJ + ii;
-        const int cb = a4_base(d, col);
-        static_for<16>([&](auto R) {
-          const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
-          acc[(int)R] = (row >= (col & ~3)) ? A[cb + row] : 0.0f;
-        });
-        static_for<16>([&](auto K2) {
-          const int k = p0 + 2 * K2 + hh;
-          const int kb = a4_base(d, k);
-          const float av = -A[kb + rI + ii];
-          const float bv = A[kb + cJ + ii];
-          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
-        });
-        static_for<16>([&](auto R) {
-          const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
-          if (row >= col) A[cb + row] = acc[(int)R];
-        });
+        while ((I + 1) * (I + 2) / 2 <= u) ++I;
+        trailing_tile(A, d, p0 - 32, q0, I + 1, u - I * (I + 1) / 2 + 1, lane);
       }
     }
     __syncthreads();
     US(3)
+    // (3) this panel's trailing update of the next column block (tiles J = 0)
+    if (p0 + 32 < d) {
+      const int mt = (d - p0 - 32) / 32;
+      if (w < mt) trailing_tile(A, d, p0, p0 + 32, w, 0, lane);
+    }
+    __syncthreads();
+    US(5)
   }
   const bool ok = okv != 0;
-  const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
-  // (4) the new factor back to the staging buffer (coalesced; the copy to
-  // out.scale and out.cov is pooled_big_post_kernel's, on all CUs) with the
-  // ok flag and gamma; then each element's as_change term replaces it in LDS
-  // (old factor read column-wise from HBM) and is summed by rows
+  // (4) the new factor back to the staging buffer (coalesced) with the ok
+  // flag, gamma and e^lam, e^lam' for pooled_big_post_kernel (all CUs), which
+  // copies it to out.scale / out.cov and forms the as_change terms
   {
     const int nA = d * (d + 4) / 2;
     f32x4* dst = (f32x4*)p.scratch;
@@ -802,67 +859,15 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     if (tid == 0) {
       ((int*)p.scratch)[nA] = ok ? 1 : 0;
       p.scratch[nA + 1] = gamma;
-    }
-  }
-  __syncthreads();
-  // four columns' old-factor loads in flight at a time
-  constexpr int NQ = (d + 63) / 64;
-#pragma unroll 1
-  for (int j0 = w; j0 < d; j0 += 4 * kUpdWaves) {
-    float lo[4][NQ];
-    static_for<4>([&](auto U) {
-      const int j = j0 + kUpdWaves * U;
-      const int64_t co = col_off(d, j);
-      static_for<NQ>([&](auto Q) {
-        const int rr = 64 * Q + lane;
-        lo[U][Q] = (j < d && rr < d - j) ? p.in.scale[co + rr] : 0.0f;
-      });
-    });
-    static_for<4>([&](auto U) {
-      const int j = j0 + kUpdWaves * U;
-      const int ab = a4_base(d, j);
-      static_for<NQ>([&](auto Q) {
-        const int rr = 64 * Q + lane;
-        if (j < d && rr < d - j) {
-          const float ln = ok ? A[ab + j + rr] : lo[U][Q];
-          A[ab + j + rr] = (ln * e1) - (lo[U][Q] * e0);
-        }
-      });
-    });
-  }
-  __syncthreads();
-  US(4)
-  if (tid < d) {
-    // row r's terms in column order; eight LDS reads in flight (a zero term
-    // past the diagonal adds nothing: s >= +0)
-    const int r = tid;
-    float s = 0.0f;
-#pragma unroll 1
-    for (int j0 = 0; j0 <= r; j0 += 8) {
-      float t[8];
-      static_for<8>([&](auto U) {
-        const int j = j0 + U;
-        t[U] = (j <= r) ? A[a4_base(d, j) + r] : 0.0f;
-      });
-      static_for<8>([&](auto U) { s = fmaf(t[U], t[U], s); });
-    }
-    rowpart[r] = s;
-  }
-  __syncthreads();
-  US(5)
-  if (w == 0) {
-    float sl[4];
-    static_for<4>([&](auto K) { sl[K] = Grp<64>::sum((64 * K + lane < d) ? rowpart[64 * K + lane] : 0.0f); });
-    const float asc = sqrtf((sl[0] + sl[1]) + (sl[2] + sl[3]));
-    if (lane == 0) {
+      p.scratch[nA + 2] = amh_expf(lam);
+      p.scratch[nA + 3] = amh_expf(lamn);
       p.out.i[0] = itr;
       p.out.mean_accept_prob[0] = maccn;
       p.out.log_step_size[0] = lamn;
-      p.out.as_change[0] = asc;
     }
   }
   if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
-  US(6)
+  US(4)
   US_FLUSH
 }
 
@@ -878,6 +883,7 @@ __global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams
   const double g = (double)amh_lr_gamma(n, p.a);
   const int64_t co = col_off(d, k);
   const int ab = a4_base(d, k);
+  if (k == 0 && threadIdx.x == 0) ((int*)p.scratch)[d * (d + 4) / 2 + 4] = it + p.K;  // the next step's i (noise blocks)
   for (int rr = threadIdx.x; rr < d - k; rr += 256) {
     const double a = (1.0 - g) * p.in.cov[co + rr];
     const double b = g * (p.sums[d + co + rr] / N);
@@ -886,30 +892,59 @@ __global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams
 }
 
 // out.scale = the new factor (or the kept one), out.cov = Sigma' (or the kept
-// one); element-wise, in-place safe (block k = column k; all CUs)
+// one); element-wise, in-place safe (block k = column k; all CUs).  Column
+// k's as_change terms t_rk = L'_rk e^lam' - L_rk e^lam (arwmh.py:197) are
+// squared and summed over the column's rows r = k + t by the 256-thread
+// big_sum order (four 64-lane butterflies, (s0 + s1) + (s2 + s3)); the column
+// sums go to the staging buffer for pooled_big_asc_kernel.
 __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams p) {
   const int d = p.d;
   const int k = blockIdx.x;
+  const int t = threadIdx.x;
+  const int nA = d * (d + 4) / 2;
   const int64_t P = (int64_t)d * (d + 1) / 2;
-  // ok flag and gamma from the update kernel (p.in.i may alias p.out.i, which
-  // the update kernel has already advanced)
-  const bool ok = ((const int*)p.scratch)[d * (d + 4) / 2] != 0;
-  const double g = (double)p.scratch[d * (d + 4) / 2 + 1];
+  __shared__ float wsum[4];
+  // ok flag, gamma, e^lam, e^lam' from the update kernel (p.in may alias
+  // p.out, which the update kernel has already advanced)
+  const bool ok = ((const int*)p.scratch)[nA] != 0;
+  const double g = (double)p.scratch[nA + 1];
+  const float e0 = p.scratch[nA + 2], e1 = p.scratch[nA + 3];
   const double N = p.sums[d + P + 1];
   const int64_t co = col_off(d, k);
   const int ab = a4_base(d, k);
-  for (int rr = threadIdx.x; rr < d - k; rr += 256) {
-    const int64_t o = co + rr;
+  float sq = 0.0f;
+  if (t < d - k) {  // d <= 256: one element per thread
+    const int64_t o = co + t;
+    const float lo = p.in.scale[o];
+    const float ln = ok ? p.scratch[ab + k + t] : lo;
+    const float tt = (ln * e1) - (lo * e0);
+    sq = tt * tt;
     if (ok) {
       const double a = (1.0 - g) * p.in.cov[o];
       const double b = g * (p.sums[d + o] / N);
       p.out.cov[o] = a + b;
-      p.out.scale[o] = p.scratch[ab + k + rr];
+      p.out.scale[o] = ln;
     } else {
       p.out.cov[o] = p.in.cov[o];
-      p.out.scale[o] = p.in.scale[o];
+      p.out.scale[o] = lo;
     }
   }
+  const float ws = Grp<64>::sum(sq);
+  if ((t & 63) == 0) wsum[t >> 6] = ws;
+  __syncthreads();
+  if (t == 0) p.scratch[nA + 8 + k] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+}
+
+// as_change = sqrtf(big_sum of the column sums) (one block)
+__global__ __launch_bounds__(256) void pooled_big_asc_kernel(PooledUpdateParams p) {
+  const int d = p.d;
+  const int t = threadIdx.x;
+  const int nA = d * (d + 4) / 2;
+  __shared__ float wsum[4];
+  const float ws = Grp<64>::sum(t < d ? p.scratch[nA + 8 + t] : 0.0f);
+  if ((t & 63) == 0) wsum[t >> 6] = ws;
+  __syncthreads();
+  if (t == 0) p.out.as_change[0] = sqrtf((wsum[0] + wsum[1]) + (wsum[2] + wsum[3]));
 }
 
 // --------------------------------------------------------------- launchers --
@@ -972,10 +1007,17 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
   hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  unsigned nblk = 1;  // + one noise block per other CU when the next step's noise is drawn ahead
+  if (p.noise_C > 0 && p.xi != nullptr) {
+    int dev = 0, cus = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    nblk = (unsigned)(cus > 1 ? cus : 2);
+  }
   switch (p.d / 32) {
 #define AMH_UPD(NT_)                                                                                    \
   case NT_:                                                                                            \
-    hipLaunchKernelGGL(pooled_big_update_kernel<NT_>, dim3(1), dim3(64 * kUpdWaves), shm, s, p);       \
+    hipLaunchKernelGGL(pooled_big_update_kernel<NT_>, dim3(nblk), dim3(64 * kUpdWaves), shm, s, p);    \
     break;
     AMH_UPD(2) AMH_UPD(3) AMH_UPD(4) AMH_UPD(5) AMH_UPD(6) AMH_UPD(7) AMH_UPD(8)
 #undef AMH_UPD
@@ -985,6 +1027,9 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_big_post_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
+  e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(pooled_big_asc_kernel, dim3(1), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

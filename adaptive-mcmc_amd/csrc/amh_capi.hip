@@ -30,6 +30,11 @@ struct amh_handle {
   float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
   size_t upd_bytes = 0;
   float* xpack = nullptr;      // diamonds: design matrix in MFMA tile order (made by amh_bind_model)
+  float* noise_buf = nullptr;  // pooled d > 64: [cap] records (i, key0, key1, u bits) then xi [cap][d]
+  size_t noise_bytes = 0;
+  int64_t noise_cap = 0;       // chains the noise buffer holds
+  int64_t noise_C = 0;         // chains of the last stats call, whose keys are at noise_keys
+  const uint32_t* noise_keys = nullptr;
   std::string err;
 };
 
@@ -150,6 +155,7 @@ int amh_destroy(amh_handle* h) {
     if (h->split_buf) (void)hipFree(h->split_buf);
     if (h->upd_buf) (void)hipFree(h->upd_buf);
     if (h->xpack) (void)hipFree(h->xpack);
+    if (h->noise_buf) (void)hipFree(h->noise_buf);
   }
   delete h;
   return AMH_OK;
@@ -560,6 +566,23 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
     h->big_ready_C = -1;
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;
+    if (d != 64) {
+      // noise drawn ahead by the update launch (records checked per chain
+      // by the stats kernel, so a stale or foreign buffer is never used)
+      const size_t nn = (size_t)num_chains * (16 + (size_t)d * sizeof(float));
+      if (nn > h->noise_bytes) {
+        rc = grow(h, &h->noise_buf, &h->noise_bytes, nn, stream, "amh_pooled_stats/hipMalloc");
+        if (rc != AMH_OK) return rc;
+        h->noise_cap = num_chains;
+        e = hipMemsetAsync(h->noise_buf, 0xFF, (size_t)num_chains * 16, (hipStream_t)stream);  // i = -1: no match
+        if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipMemsetAsync");
+      }
+      p.xrec = (const uint4*)h->noise_buf;
+      p.xi = h->noise_buf + 4 * h->noise_cap;
+      p.xi_cap = h->noise_cap;
+      h->noise_C = num_chains;
+      h->noise_keys = in->rng_key;
+    }
     // one launch sequence per step of the block, the sums accumulated
     for (int32_t t = 0; t < k_steps; ++t) {
       p.i_add = t;
@@ -602,10 +625,16 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
   p.out = *out;
   p.K = k_steps;
   if (amh::pooled_big_model(h->model_id, p.d)) {
-    const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 4) * sizeof(float);
+    const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 8 + (size_t)p.d) * sizeof(float);
     int rc = grow(h, &h->upd_buf, &h->upd_bytes, need, stream, "amh_pooled_update/hipMalloc");
     if (rc != AMH_OK) return rc;
     p.scratch = h->upd_buf;
+    if (p.d != 64 && h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys) {
+      p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows
+      p.keys = (const uint32_t*)in->rng_key;
+      p.xrec = (uint4*)h->noise_buf;
+      p.xi = h->noise_buf + 4 * h->noise_cap;
+    }
     e = amh::run_pooled_big_update(p, (hipStream_t)stream);
   } else {
     e = amh::run_pooled_update(p, (hipStream_t)stream);

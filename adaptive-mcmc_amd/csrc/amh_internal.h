@@ -100,6 +100,12 @@ struct PooledStatsParams {
   int32_t k_steps;     // d <= 64: transitions per chain with the frozen shared state
   int32_t i_add;       // d > 64: this launch is step i + i_add of the block
   int32_t accumulate;  // d > 64: sums += this launch's sums (steps after the first)
+  // d > 64: noise made ahead of time (pooled_big_update_kernel's extra
+  // blocks): xi [cap][d] and per-chain records (i, key0, key1, u bits); a
+  // chain uses them only if its record matches (i, its key), else it draws
+  const float* xi;
+  const uint4* xrec;
+  int64_t xi_cap;
 };
 
 // Pool-every-K: the update after a block of K transitions that started at
@@ -114,8 +120,14 @@ struct PooledUpdateParams {
   float a, target;
   const double* sums;
   amh_pooled_state in, out;
-  float* scratch;  // d > 64: d(d+4)/2 floats (4-row-aligned factor) + ok flag
+  float* scratch;  // d >= 64: d(d+4)/2 floats (4-row-aligned factor), ok, gamma, e^lam, e^lam', 4 spare, d column sums
   int32_t K;       // transitions per pooled update (the sums cover K * C chain-steps)
+  // d > 64: the next step's noise for chains [0, noise_C) is drawn by the
+  // update launch's extra blocks into xi / xrec (PooledStatsParams)
+  int64_t noise_C;
+  const uint32_t* keys;
+  float* xi;
+  uint4* xrec;
 };
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);

@@ -224,7 +224,11 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
 // pooled_final_kernel adds them in group order.
 constexpr int kRedGroup = 16;
 
-__global__ __launch_bounds__(256) void pooled_group_kernel(const double* __restrict__ partials, int64_t n_chunks,
+// T = float: the large-d stats kernel's partials, which are float32 sums
+// (their conversion to double is exact, so storing them as float halves the
+// traffic and changes no bit)
+template <typename T>
+__global__ __launch_bounds__(256) void pooled_group_kernel(const T* __restrict__ partials, int64_t n_chunks,
                                                            int64_t V, double* __restrict__ gsum) {
   const int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x;
   const int64_t g = blockIdx.y;
@@ -232,7 +236,7 @@ __global__ __launch_bounds__(256) void pooled_group_kernel(const double* __restr
   const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
   double x[kRedGroup];
 #pragma unroll
-  for (int q = 0; q < kRedGroup; ++q) x[q] = (g * kRedGroup + q < c1) ? partials[(g * kRedGroup + q) * V + v] : 0.0;
+  for (int q = 0; q < kRedGroup; ++q) x[q] = (g * kRedGroup + q < c1) ? (double)partials[(g * kRedGroup + q) * V + v] : 0.0;
   double s = 0.0;  // chunk order; a missing tail chunk adds nothing (it is not added at all)
 #pragma unroll
   for (int q = 0; q < kRedGroup; ++q)
@@ -284,7 +288,12 @@ hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, do
   const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
   double* gsum = const_cast<double*>(partials) + n_chunks * V;
   const unsigned vb = (unsigned)((V + 255) / 256);
-  hipLaunchKernelGGL(pooled_group_kernel, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials, n_chunks, V, gsum);
+  if (tile_d)  // the large-d stats kernel's float32 partials
+    hipLaunchKernelGGL(pooled_group_kernel<float>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s,
+                       (const float*)partials, n_chunks, V, gsum);
+  else
+    hipLaunchKernelGGL(pooled_group_kernel<double>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials,
+                       n_chunks, V, gsum);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_final_kernel, dim3(vb), dim3(256), 0, s, (const double*)gsum, n_groups, V, sums,

@@ -1119,8 +1119,8 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
  *            adds), written in double; chunks reduced as in the d <= 64 mode.
  *  update    Sigma' in double as the d <= 64 mode; its Cholesky factor in
  *            float32 (element (r, k) updated in column order j < k, then
- *            divided by L_kk = sqrtf(A_kk)); as_change per row sequential,
- *            rows by big_sum. */
+ *            divided by L_kk = sqrtf(A_kk)); as_change: squared terms of
+ *            column j (rows j + t) by big_sum, then the columns by big_sum. */
 /* chains per chunk: 64 at d = 64 (pooled_fused64_kernel), 128 above
  * (pooled_fused_big_kernel: one chunk per block iteration, two 64-chain halves) */
 static int64_t orc_big_chunk(int d) { return d == 64 ? 64 : 128; }
@@ -1235,15 +1235,19 @@ static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t
   }
   const float e0 = amh_expf(*lam), e1 = amh_expf(lamn);
   float part[ORC_BIG];
-  for (int r = 0; r < d; ++r) {
-    float sacc = 0.0f;
-    for (int j = 0; j <= r; ++j) {
-      const float lo = Lpacked[col_off(d, j) + (r - j)];
-      const float ln = ok ? A[r * d + j] : lo;
-      const float tt = (ln * e1) - (lo * e0);
-      sacc = fmaf(tt, tt, sacc);
+  for (int j = 0; j < d; ++j) {  /* column j's squared terms, rows j + t, big_sum order */
+    float col[ORC_BIG];
+    for (int t = 0; t < d; ++t) {
+      col[t] = 0.0f;
+      if (t < d - j) {
+        const int r = j + t;
+        const float lo = Lpacked[col_off(d, j) + (r - j)];
+        const float ln = ok ? A[r * d + j] : lo;
+        const float tt = (ln * e1) - (lo * e0);
+        col[t] = tt * tt;
+      }
     }
-    part[r] = sacc;
+    part[j] = big_sum(col, d);
   }
   *asc = sqrtf(big_sum(part, d));
   if (ok) {

@@ -226,3 +226,34 @@ def test_pooled_two_ranks(d, C, steps, K, overlap, world, gpu, tmp_path):
     # under the other association order; allow a handful of such chains
     zd = np.abs(r["z"] - st.z.cpu().numpy()).max(axis=1) > 1e-4 * (1 + np.abs(r["z"]).max(axis=1))
     assert zd.sum() <= max(2, C // 1000), zd.sum()
+
+
+@pytest.mark.parametrize("d,C", [(128, 700), (256, 300)])
+def test_pooled_noise_ahead_invalidation(d, C, gpu, orc):
+    """Above d = 64 the update launch draws the next step's noise ahead of
+    time; each chain's record (i, key) decides whether the stats kernel may
+    use it.  Editing the keys or the counter between steps must fall back to
+    drawing, bit for bit against the oracle."""
+    from kernels_amd import PooledARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", d)
+    k = PooledARWMH(num_chains=C, **kw)
+    z0 = np.random.default_rng(9).uniform(-2, 2, size=(C, d)).astype(np.float32)
+    st = k.init(PRNGKey(9), 0, torch.as_tensor(z0), (), mk)
+    ost = orc.init(om, PRNGKey(9), C, init_z=z0)
+    z, pe, keys = ost.z, ost.potential_energy, ost.rng_key.copy()
+    sh = orc.pooled_init_shared(d)
+    for t in range(6):
+        if t == 2:  # rotate the keys of the first 37 chains in place
+            kk = st.rng_key[:37].clone()
+            st.rng_key[:37] = torch.roll(kk, 1, dims=0)
+            keys[:37] = np.roll(keys[:37].copy(), 1, axis=0)
+        if t == 4:  # rewind the shared counter: records of i + 1 no longer match
+            st.i.sub_(1)
+            sh["i"] = sh["i"] - 1
+        st = k.sample(st)
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        orc.pooled_update(om, sums, sh)
+        torch.cuda.synchronize()
+        assert st.z.cpu().numpy().tobytes() == z.tobytes(), f"z differs at step {t + 1}"
+        assert st.adapt_state.scale.cpu().numpy().tobytes() == np.asarray(sh["L"]).tobytes(), f"L at step {t + 1}"
+        assert st.as_change.cpu().numpy().tobytes() == np.asarray(sh["asc"]).astype(np.float32).tobytes()

@@ -1,7 +1,8 @@
 """Phase breakdown of the pooled large-d update kernel (diagnostic build,
 make -C adaptive-mcmc_amd/csrc stamps): s_memtime totals of thread 0 for
-init / diagonal blocks / panel solves / trailing updates / write-out /
-as_change rows / final reduction.  Usage (GPU box):
+init / panel columns / panel loads / the barrier behind the look-ahead
+trailing update / write-out / the next column block's update / panel
+write-back.  Usage (GPU box):
   python3 tools/upd_stamps.py [--dim 256] [--chains 32768]
 """
 import argparse
@@ -34,8 +35,8 @@ buf = np.zeros(8, np.uint64)
 L = _lib.lib()
 L.amh_diag_upd_stamps.argtypes = [ctypes.c_void_p]
 assert L.amh_diag_upd_stamps(buf.ctypes.data) == 0
-names = ["init", "panel columns", "panel loads + barrier", "trailing", "write-out", "as_change rows", "final",
-         "panel write-back"]
+names = ["init", "panel columns", "panel loads", "look-ahead barrier", "write-out", "next column block",
+         "(unused)", "panel write-back"]
 tot = buf[:8].sum()
 for n, v in zip(names, buf[:8]):
     print(f"{n:15s} {int(v):9d} ticks  {100.0 * v / tot:5.1f} %")
