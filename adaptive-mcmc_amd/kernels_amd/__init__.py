@@ -14,7 +14,8 @@ from .arwmh import ARWMH, ARWMHAdaptState, ARWMHState, init_to_uniform, pack_sca
 from .asss import ASSS, ASSSAdaptState, ASSSState
 from .pooled import PooledAdaptState, PooledARWMH, PooledState
 from .random import PRNGKey, split
+from .checkpoint import load_state, load_state_dict, save_state, state_dict
 
 __all__ = ["ARWMH", "ARWMHState", "ARWMHAdaptState", "init_to_uniform", "pack_scale", "unpack_scale",
            "packed_size", "PRNGKey", "split", "PooledARWMH", "PooledState", "PooledAdaptState",
-           "ASSS", "ASSSState", "ASSSAdaptState"]
+           "ASSS", "ASSSState", "ASSSAdaptState", "state_dict", "load_state_dict", "save_state", "load_state"]

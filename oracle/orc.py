@@ -17,7 +17,9 @@ from dataclasses import dataclass
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "build", "libamh_oracle.so")
+# AMH_ORACLE_LIB selects another build of the same source (the sanitizer build,
+# `make -C oracle asan`, run by tests/test_oracle_asan.py)
+_LIB_PATH = os.environ.get("AMH_ORACLE_LIB") or os.path.join(_HERE, "build", "libamh_oracle.so")
 
 GAUSSIAN, EIGHT_SCHOOLS, KIDIQ, DIAMONDS, DIAMONDS_SS = 1, 2, 3, 4, 5
 
