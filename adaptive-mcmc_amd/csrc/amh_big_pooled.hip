@@ -264,9 +264,9 @@ template <int NT>
 constexpr size_t fused_big_lds_bytes() {
   return ((size_t)2 * 32 * NT * kLd + (size_t)NT * 64 + 3 * 64 + 32 * NT) * sizeof(float);
 }
-int64_t pooled_big_tile_V(int d) {
+int64_t pooled_big_tile_V(int d) {  // [S_d | S_dd tiles | 2 pad | S_a | N]: a multiple of 4
   const int nt = d / 32;
-  return d + (int64_t)(nt * (nt + 1) / 2) * 1024 + 2;
+  return d + (int64_t)(nt * (nt + 1) / 2) * 1024 + 4;
 }
 int64_t pooled_big_pack_floats(int d) {
   const int nt = d / 32;
@@ -307,7 +307,7 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
                                                                int64_t n_chunks) {
   constexpr int D = 32 * NT;
   constexpr int NPAIR = NT * (NT + 1) / 2;
-  constexpr int64_t V = D + (int64_t)NPAIR * 1024 + 2;  // "tile" partial row (pooled_final_kernel maps it)
+  constexpr int64_t V = D + (int64_t)NPAIR * 1024 + 4;  // "tile" partial row (pooled_final_kernel maps it)
   constexpr int NS = (NPAIR + kFBWaves - 1) / kFBWaves;  // S_dd tile pairs per wave (<= 5)
   constexpr int NQ = (D + 63) / 64;  // coordinates per lane in the chain-major phases
   constexpr int CPW = 64 / kFBWaves;  // chains per wave in the chain-major phases
@@ -896,7 +896,7 @@ __global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams
 // k's as_change terms t_rk = L'_rk e^lam' - L_rk e^lam (arwmh.py:197) are
 // squared and summed over the column's rows r = k + t by the 256-thread
 // big_sum order (four 64-lane butterflies, (s0 + s1) + (s2 + s3)); the column
-// sums go to the staging buffer for pooled_big_asc_kernel.
+// sums are handed to the block that finishes last, which forms as_change.
 __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams p) {
   const int d = p.d;
   const int k = blockIdx.x;
@@ -932,24 +932,36 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
   const float ws = Grp<64>::sum(sq);
   if ((t & 63) == 0) wsum[t >> 6] = ws;
   __syncthreads();
-  if (t == 0) p.scratch[nA + 8 + k] = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
-}
-
-// as_change = sqrtf(big_sum of the column sums) (one block)
-__global__ __launch_bounds__(256) void pooled_big_asc_kernel(PooledUpdateParams p) {
-  const int d = p.d;
-  const int t = threadIdx.x;
-  const int nA = d * (d + 4) / 2;
-  __shared__ float wsum[4];
-  const float ws = Grp<64>::sum(t < d ? p.scratch[nA + 8 + t] : 0.0f);
-  if ((t & 63) == 0) wsum[t >> 6] = ws;
+  // the column sum goes out write-through (sc1) and the block takes a ticket;
+  // the block that takes the last one sums the columns (cross-XCD hand-off:
+  // sc1 stores, vmcnt(0), agent-scope add; sc1 loads by the last arriver)
+  uint32_t* colsum = (uint32_t*)(p.scratch + nA + 8);
+  int* ticket = (int*)p.scratch + nA + 5;
+  __shared__ int last;
+  if (t == 0) {
+    const float cs = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
+    __hip_atomic_store(&colsum[k], __float_as_uint(cs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d - 1;
+  }
   __syncthreads();
-  if (t == 0) p.out.as_change[0] = sqrtf((wsum[0] + wsum[1]) + (wsum[2] + wsum[3]));
+  if (!last) return;
+  // as_change = sqrtf(big_sum of the column sums)
+  const float v = t < d ? __uint_as_float(__hip_atomic_load(&colsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                        : 0.0f;
+  const float vs = Grp<64>::sum(v);
+  __syncthreads();  // every wave has read wsum above
+  if ((t & 63) == 0) wsum[t >> 6] = vs;
+  __syncthreads();
+  if (t == 0) {
+    p.out.as_change[0] = sqrtf((wsum[0] + wsum[1]) + (wsum[2] + wsum[3]));
+    __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+  }
 }
 
 // --------------------------------------------------------------- launchers --
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
-                         hipStream_t s, int tile_d = 0);
+                         hipStream_t s, int tile_d = 0, FinalPrep fp = FinalPrep{});
 
 // chains per chunk of the sums (bit spec): 64 at d = 64 (the fused kernel's
 // block), 256 above
@@ -998,15 +1010,18 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     (void)pep;
-    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d);
+    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d, p.prep);
   }
 }
 
-hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
+hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, bool sigma_ready) {
   const size_t shm = (size_t)p.d * (p.d + 4) / 2 * sizeof(float);
-  hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
+  hipError_t e = hipSuccess;
+  if (!sigma_ready) {  // else pooled_final_kernel formed Sigma' already
+    hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
+    e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
   unsigned nblk = 1;  // + one noise block per other CU when the next step's noise is drawn ahead
   if (p.noise_C > 0 && p.xi != nullptr) {
     int dev = 0, cus = 0;
@@ -1027,9 +1042,6 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s) {
   e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_big_post_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
-  e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(pooled_big_asc_kernel, dim3(1), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 

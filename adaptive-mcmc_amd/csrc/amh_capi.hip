@@ -518,8 +518,15 @@ int amh_pooled_sums_size(int32_t dim, int64_t* v) {
   return AMH_OK;
 }
 
-int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
-                       float* z_out, float* pe_out, double* sums, void* stream) {
+}  // extern "C"
+
+// prep_for_update: the update follows in the same library call with no
+// exchange in between (amh_pooled_step_k on one rank), so the large-d
+// reduction's last kernel also forms that update's Sigma'
+static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
+                             float* z_out, float* pe_out, double* sums, void* stream, bool prep_for_update,
+                             bool* sigma_ready) {
+  if (sigma_ready) *sigma_ready = false;
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_stats: null handle");
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
   if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1 || k_steps < 1)
@@ -582,11 +589,31 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
       p.xi_cap = h->noise_cap;
       h->noise_C = num_chains;
       h->noise_keys = in->rng_key;
+      if (prep_for_update) {  // grown here: pooled_update_impl's grow is then a no-op
+        const size_t un = ((size_t)d * (d + 4) / 2 + 8 + (size_t)d) * sizeof(float);
+        const bool fresh = un > h->upd_bytes;
+        rc = grow(h, &h->upd_buf, &h->upd_bytes, un, stream, "amh_pooled_stats/hipMalloc");
+        if (rc != AMH_OK) return rc;
+        if (fresh) {
+          e = hipMemsetAsync(h->upd_buf, 0, h->upd_bytes, (hipStream_t)stream);
+          if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipMemsetAsync");
+        }
+      }
     }
     // one launch sequence per step of the block, the sums accumulated
     for (int32_t t = 0; t < k_steps; ++t) {
       p.i_add = t;
       p.accumulate = t > 0;
+      if (prep_for_update && d != 64 && t == k_steps - 1) {
+        p.prep.cov = in->cov;
+        p.prep.i = in->i;
+        p.prep.scratch = h->upd_buf;
+        p.prep.N = (double)num_chains * (double)k_steps;
+        p.prep.W = h->cfg.num_warmup;
+        p.prep.K = k_steps;
+        p.prep.a = h->cfg.lr_decay;
+        if (sigma_ready) *sigma_ready = true;
+      }
       if (t > 0) {
         p.z = z_out;
         p.pe = pe_out;
@@ -602,6 +629,16 @@ int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state
   return AMH_OK;
 }
 
+static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
+                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready);
+
+extern "C" {
+
+int amh_pooled_stats_k(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
+                       float* z_out, float* pe_out, double* sums, void* stream) {
+  return pooled_stats_impl(h, num_chains, in, k_steps, z_out, pe_out, sums, stream, false, nullptr);
+}
+
 int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, float* z_out, float* pe_out,
                      double* sums, void* stream) {
   return amh_pooled_stats_k(h, num_chains, in, 1, z_out, pe_out, sums, stream);
@@ -609,6 +646,13 @@ int amh_pooled_stats(amh_handle* h, int64_t num_chains, const amh_pooled_state* 
 
 int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
                         int32_t k_steps, void* stream) {
+  return pooled_update_impl(h, sums, in, out, k_steps, stream, false);
+}
+
+}  // extern "C"
+
+static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
+                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_update: null handle");
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
   if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
@@ -626,8 +670,13 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
   p.K = k_steps;
   if (amh::pooled_big_model(h->model_id, p.d)) {
     const size_t need = ((size_t)p.d * (p.d + 4) / 2 + 8 + (size_t)p.d) * sizeof(float);
+    const bool fresh = need > h->upd_bytes;
     int rc = grow(h, &h->upd_buf, &h->upd_bytes, need, stream, "amh_pooled_update/hipMalloc");
     if (rc != AMH_OK) return rc;
+    if (fresh) {  // the post kernel's arrival ticket starts at zero (its last block resets it)
+      e = hipMemsetAsync(h->upd_buf, 0, h->upd_bytes, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipMemsetAsync");
+    }
     p.scratch = h->upd_buf;
     if (p.d != 64 && h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys) {
       p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows
@@ -635,13 +684,15 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
       p.xrec = (uint4*)h->noise_buf;
       p.xi = h->noise_buf + 4 * h->noise_cap;
     }
-    e = amh::run_pooled_big_update(p, (hipStream_t)stream);
+    e = amh::run_pooled_big_update(p, (hipStream_t)stream, sigma_ready);
   } else {
     e = amh::run_pooled_update(p, (hipStream_t)stream);
   }
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update");
   return AMH_OK;
 }
+
+extern "C" {
 
 int amh_pooled_update(amh_handle* h, const double* sums, const amh_pooled_state* in, const amh_pooled_state* out,
                       void* stream) {
@@ -654,9 +705,11 @@ int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state*
     return fail(h, AMH_EINVAL, "amh_pooled_step: n_steps must be a non-negative multiple of sync_every");
   const amh_pooled_state* src = in;
   for (int32_t t = 0; t < n_steps; t += sync_every) {
-    int rc = amh_pooled_stats_k(h, num_chains, src, sync_every, out->z, out->potential_energy, sums, stream);
+    bool ready = false;  // one rank, no exchange: the reduction also forms Sigma'
+    int rc = pooled_stats_impl(h, num_chains, src, sync_every, out->z, out->potential_energy, sums, stream, true,
+                               &ready);
     if (rc != AMH_OK) return rc;
-    rc = amh_pooled_update_k(h, sums, src, out, sync_every, stream);
+    rc = pooled_update_impl(h, sums, src, out, sync_every, stream, ready);
     if (rc != AMH_OK) return rc;
     src = out;
   }

@@ -86,6 +86,19 @@ __host__ __device__ inline int pooled_cpw(int64_t C) {
   return c < 1 ? 1 : (c > 16 ? 16 : (int)c);
 }
 
+// pooled_final_kernel may also form the large-d update's Sigma' (what
+// pooled_big_prep_kernel does) when the update follows in the same library
+// call with no exchange in between (amh_pooled_step_k, one rank): scratch
+// non-null, N = the chain-steps the sums cover
+struct FinalPrep {
+  const double* cov;
+  const int32_t* i;
+  float* scratch;
+  double N;
+  int32_t W, K;
+  float a;
+};
+
 struct PooledStatsParams {
   int64_t C;
   int32_t d;
@@ -106,6 +119,7 @@ struct PooledStatsParams {
   const float* xi;
   const uint4* xrec;
   int64_t xi_cap;
+  FinalPrep prep;  // scratch == nullptr: none
 };
 
 // Pool-every-K: the update after a block of K transitions that started at
@@ -137,7 +151,7 @@ int64_t pooled_big_pack_floats(int d);
 int64_t pooled_big_tile_V(int d);  // partial row length of the fused large-d stats (d > 64)  // scratch floats of the fused large-d stats (A-operand tiles)
 int64_t pooled_scratch_rows(int64_t n_chunks);  // partials + group sums of pooled_reduce
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
-hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s);
+hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, bool sigma_ready = false);
 hipError_t run_asss_step(int model_id, const StepParams& p, hipStream_t s);  // amh_asss.hip
 hipError_t run_asss_pnx(int model_id, const AsssPnxParams& p, hipStream_t s);
 // evaluation metrics (amh_eval.hip)

@@ -244,14 +244,44 @@ __global__ __launch_bounds__(256) void pooled_group_kernel(const T* __restrict__
   gsum[g * V + v] = s;
 }
 
+// the large-d stats kernel's float32 partials (their widening to double is
+// exact, so storing them as float halves the traffic and changes no bit),
+// four consecutive entries per thread (V % 4 == 0: the tile row is padded)
+__global__ __launch_bounds__(256) void pooled_group4_kernel(const float* __restrict__ partials, int64_t n_chunks,
+                                                            int64_t V, double* __restrict__ gsum) {
+  const int64_t v4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t g = blockIdx.y;
+  if (4 * v4 >= V) return;
+  const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
+  float4 x[kRedGroup];
+#pragma unroll
+  for (int q = 0; q < kRedGroup; ++q)
+    x[q] = (g * kRedGroup + q < c1) ? ((const float4*)(partials + (g * kRedGroup + q) * V))[v4] : float4{};
+  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;  // chunk order
+#pragma unroll
+  for (int q = 0; q < kRedGroup; ++q)
+    if (g * kRedGroup + q < c1) {
+      s0 += (double)x[q].x;
+      s1 += (double)x[q].y;
+      s2 += (double)x[q].z;
+      s3 += (double)x[q].w;
+    }
+  double* o = gsum + g * V + 4 * v4;
+  o[0] = s0;
+  o[1] = s1;
+  o[2] = s2;
+  o[3] = s3;
+}
+
 // Row u of a "tile" partial (pooled_fused_big_kernel, d > 64): [d S_d | NPAIR
 // 32x32 tiles of S_dd in MFMA register order (pair, reg R, lane) | S_a | N]
 // -> its index in the packed sums vector (-1: above the diagonal of a
 // diagonal tile, not part of the sums).
-__device__ int64_t tile_to_packed(int64_t u, int64_t Vt, int d) {
+__device__ int64_t tile_to_packed(int64_t u, int64_t Vt, int d, int* prow = nullptr, int* pcol = nullptr) {
   const int64_t P = (int64_t)d * (d + 1) / 2;
   if (u < d) return u;
   if (u >= Vt - 2) return u - Vt + d + P + 2;
+  if (u >= Vt - 4) return -1;  // padding (V % 4 == 0)
   const int64_t q = u - d;
   const int pair = (int)(q >> 10), R = (int)((q >> 6) & 15), lane = (int)(q & 63);
   int I = 0;
@@ -259,14 +289,23 @@ __device__ int64_t tile_to_packed(int64_t u, int64_t Vt, int d) {
   const int J = pair - I * (I + 1) / 2;
   const int row = 32 * I + (R & 3) + 8 * (R >> 2) + 4 * (lane >> 5), col = 32 * J + (lane & 31);
   if (row < col) return -1;
+  if (prow) *prow = row;
+  if (pcol) *pcol = col;
   return d + (int64_t)col * d - (int64_t)col * (col - 1) / 2 + (row - col);
 }
 
+// the update's 4-row-aligned layout (amh_big_pooled.hip a4_base)
+__device__ __forceinline__ int fp_a4_base(int d, int j) {
+  const int q = j >> 2;
+  return 4 * (q * d - 2 * q * (q - 1)) + (j & 3) * (d - 4 * q) - (j & ~3);
+}
+
 __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
-                                                           double* sums, int accumulate, int tile_d) {
+                                                           double* sums, int accumulate, int tile_d, FinalPrep fp) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (u >= V) return;
-  const int64_t v = tile_d ? tile_to_packed(u, V, tile_d) : u;
+  int row = -1, col = -1;
+  const int64_t v = tile_d ? tile_to_packed(u, V, tile_d, &row, &col) : u;
   if (v < 0) return;
   double tot = 0.0;
   int64_t g = 0;
@@ -278,26 +317,38 @@ __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restr
     for (int q = 0; q < 8; ++q) tot += x[q];
   }
   for (; g < n_groups; ++g) tot += gsum[g * V + u];
-  sums[v] = accumulate ? sums[v] + tot : tot;
+  const double sv = accumulate ? sums[v] + tot : tot;
+  sums[v] = sv;
+  if (fp.scratch != nullptr && col >= 0) {
+    // Sigma' = (1-g) Sigma + g S_dd / N in float, as pooled_big_prep_kernel
+    const int d = tile_d;
+    const int32_t it = fp.i[0];
+    const double gm = (double)amh_lr_gamma(pooled_block_n(it, fp.W, fp.K), fp.a);
+    const int64_t o = v - d;
+    const double a = (1.0 - gm) * fp.cov[o];
+    const double b = gm * (sv / fp.N);
+    fp.scratch[fp_a4_base(d, col) + row] = (float)(a + b);
+    if (u == d) ((int*)fp.scratch)[d * (d + 4) / 2 + 4] = it + fp.K;  // the next step's i (noise blocks)
+  }
 }
 
 int64_t pooled_scratch_rows(int64_t n_chunks) { return n_chunks + (n_chunks + kRedGroup - 1) / kRedGroup; }
 
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
-                         hipStream_t s, int tile_d = 0) {
+                         hipStream_t s, int tile_d = 0, FinalPrep fp = FinalPrep{}) {
   const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
   double* gsum = const_cast<double*>(partials) + n_chunks * V;
   const unsigned vb = (unsigned)((V + 255) / 256);
-  if (tile_d)  // the large-d stats kernel's float32 partials
-    hipLaunchKernelGGL(pooled_group_kernel<float>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s,
-                       (const float*)partials, n_chunks, V, gsum);
+  if (tile_d)  // the large-d stats kernel's float32 partials, V % 4 == 0
+    hipLaunchKernelGGL(pooled_group4_kernel, dim3((unsigned)((V / 4 + 255) / 256), (unsigned)n_groups), dim3(256), 0,
+                       s, (const float*)partials, n_chunks, V, gsum);
   else
     hipLaunchKernelGGL(pooled_group_kernel<double>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials,
                        n_chunks, V, gsum);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_final_kernel, dim3(vb), dim3(256), 0, s, (const double*)gsum, n_groups, V, sums,
-                     accumulate, tile_d);
+                     accumulate, tile_d, fp);
   return hipGetLastError();
 }
 
