@@ -345,8 +345,11 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
   });
 
   for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
-    f32x16 sacc[NS];
-    static_for<NS>([&](auto S) { sacc[S] = f32x16{}; });
+    // float32 partials (pooled_group4_kernel widens them exactly); the S_dd
+    // accumulators live in registers only during (6): after each half they
+    // are parked in the chunk's own partial row (tile / register order) and
+    // the next half continues from them, so (1)-(5) keep their registers
+    float* out = (float*)p.partials + chunk * V;
     float sd = 0.0f, sa = 0.0f;
     int cnt = 0;
 #pragma unroll 1
@@ -426,21 +429,34 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
           const int T = pT;
           f32x16 acc0 = f32x16{}, acc1 = f32x16{};
           const f32x4* a = LP + (T * (T + 1) / 2) * 256 + lane;
-          f32x4 cur[4], nxt[4];
-          static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
-          #ifndef AMH_FB_NOPROP
-#pragma unroll 1
-          for (int J = 0; J <= T; ++J) {
-            if (J < T) static_for<4>([&](auto KB) { nxt[KB] = a[256 * (J + 1) + 64 * KB]; });
+#ifndef AMH_FB_NOPROP
+          // the next A tile is prefetched unconditionally (a conditional load
+          // is sunk next to its use); the B operands of a tile are read in
+          // one batch ahead of its MFMAs
+          auto tile = [&](const f32x4 (&at)[4], int J) {
             const float* xb = Xb + (32 * J + h) * kLd + i;
+            float b0[16], b1[16];
+            static_for<16>([&](auto Q) {
+              b0[Q] = xb[2 * Q * kLd];
+              b1[Q] = xb[2 * Q * kLd + 32];
+            });
+            __builtin_amdgcn_sched_barrier(0);
             static_for<4>([&](auto KB) {
               static_for<4>([&](auto E) {
-                const int ko = 8 * KB + 2 * E;
-                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], xb[ko * kLd], acc0, 0, 0, 0);
-                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], xb[ko * kLd + 32], acc1, 0, 0, 0);
+                acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(at[KB][(int)E], b0[4 * KB + E], acc0, 0, 0, 0);
+                acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(at[KB][(int)E], b1[4 * KB + E], acc1, 0, 0, 0);
               });
             });
-            if (J < T) static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
+          };
+          f32x4 cur[4], nxt[4];
+          static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
+#pragma unroll 1
+          for (int J = 0; J <= T; ++J) {
+            const f32x4* an = a + 256 * (J < T ? J + 1 : T);  // unconditional prefetch (the last re-reads T)
+            static_for<4>([&](auto KB) { nxt[KB] = an[64 * KB]; });
+            tile(cur, J);
+            __builtin_amdgcn_sched_barrier(0);  // the hand-over stays behind the MFMAs
+            static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
           }
 #endif
           static_for<16>([&](auto R) {
@@ -470,21 +486,31 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
         const int T = qT;
         f32x16 acc0 = f32x16{}, acc1 = f32x16{};
         const f32x4* a = PP + (T * NT) * 256 + lane;
-        f32x4 cur[4], nxt[4];
-        static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
-        #ifndef AMH_FB_NOPOT
-#pragma unroll 1
-        for (int J = 0; J < NT; ++J) {
-          if (J + 1 < NT) static_for<4>([&](auto KB) { nxt[KB] = a[256 * (J + 1) + 64 * KB]; });
+#ifndef AMH_FB_NOPOT
+        auto tile = [&](const f32x4 (&at)[4], int J) {
           const float* zb = Zb + (32 * J + h) * kLd + i;
+          float b0[16], b1[16];
+          static_for<16>([&](auto Q) {
+            b0[Q] = zb[2 * Q * kLd];
+            b1[Q] = zb[2 * Q * kLd + 32];
+          });
+          __builtin_amdgcn_sched_barrier(0);
           static_for<4>([&](auto KB) {
             static_for<4>([&](auto E) {
-              const int ko = 8 * KB + 2 * E;
-              acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], zb[ko * kLd], acc0, 0, 0, 0);
-              acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(cur[(int)KB][(int)E], zb[ko * kLd + 32], acc1, 0, 0, 0);
+              acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(at[KB][(int)E], b0[4 * KB + E], acc0, 0, 0, 0);
+              acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(at[KB][(int)E], b1[4 * KB + E], acc1, 0, 0, 0);
             });
           });
-          if (J + 1 < NT) static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
+        };
+        f32x4 cur[4], nxt[4];
+        static_for<4>([&](auto KB) { cur[KB] = a[64 * KB]; });
+#pragma unroll 1
+        for (int J = 0; J < NT; ++J) {
+          const f32x4* an = a + 256 * (J + 1 < NT ? J + 1 : NT - 1);  // unconditional prefetch
+          static_for<4>([&](auto KB) { nxt[KB] = an[64 * KB]; });
+          tile(cur, J);
+          __builtin_amdgcn_sched_barrier(0);  // the hand-over stays behind the MFMAs
+          static_for<4>([&](auto KB) { cur[KB] = nxt[KB]; });
         }
 #endif
         float ps0 = 0.0f, ps1 = 0.0f;
@@ -560,6 +586,18 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
         for (int c = 0; c < nv; ++c) sa = sa + alph[c];
       }
       cnt += nv;
+      {
+      int lq_ = lane;
+      asm volatile("" : "+v"(lq_));
+      f32x16 sacc[NS];
+      static_for<NS>([&](auto S) {
+        if (half == 0 || sI[S] < 0) {
+          sacc[S] = f32x16{};
+        } else {
+          const float* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lq_;
+          static_for<16>([&](auto R) { sacc[S][(int)R] = o[64 * R]; });
+        }
+      });
 #ifndef AMH_FB_NOSDD
       static_for<NS>([&](auto S) {
         if (sI[S] >= 0) {
@@ -579,23 +617,21 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
         }
       });
 #endif
+      // S_dd tiles in register order: one coalesced 256-B row per register
+      // (the final values after the chunk's last half)
+      static_for<NS>([&](auto S) {
+        if (sI[S] >= 0) {
+          float* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lq_;
+          static_for<16>([&](auto R) { o[64 * R] = sacc[S][(int)R]; });
+        }
+      });
+      }
     }
-    // float32 partials (pooled_group_kernel<float> widens them exactly)
-    float* out = (float*)p.partials + chunk * V;
-    int lo_ = lane;
-    asm volatile("" : "+v"(lo_));
     if (tid < D) out[tid] = sd;
     if (tid == 64 * kFBWaves - 1) {
       out[V - 2] = sa;
       out[V - 1] = (float)cnt;
     }
-    // S_dd tiles in register order: one coalesced 256-B row per register
-    static_for<NS>([&](auto S) {
-      if (sI[S] >= 0) {
-        float* o = out + D + (int64_t)(w + kFBWaves * S) * 1024 + lo_;
-        static_for<16>([&](auto R) { o[64 * R] = sacc[S][(int)R]; });
-      }
-    });
   }
 }
 
