@@ -599,23 +599,40 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
         }
       });
 #ifndef AMH_FB_NOSDD
-      static_for<NS>([&](auto S) {
-        if (sI[S] >= 0) {
-          const int ra = (32 * sI[S] + i) * kLd, rb = (32 * sJ[S] + i) * kLd;
-          int kk = 0;
+      {
+        // all of the wave's tile pairs per 8-chain block: the block's
+        // operands read in one LDS batch, then the pairs' MFMAs interleaved
+        // (independent accumulators); each accumulator still takes the
+        // chains in order
+        int ra[NS], rb[NS];
+        static_for<NS>([&](auto S) {
+          ra[S] = (32 * (sI[S] >= 0 ? sI[S] : 0) + i) * kLd;
+          rb[S] = (32 * (sI[S] >= 0 ? sJ[S] : 0) + i) * kLd;
+        });
+        const bool lastS = sI[NS - 1] >= 0;  // wave-uniform: the last pair may be absent
+        int kk = 0;
 #pragma unroll 1
-          for (; kk + 16 <= nv; kk += 16) {
-            float a[8], b[8];
-            static_for<8>([&](auto Q) {
-              a[Q] = Zb[ra + kk + 2 * Q + h];
-              b[Q] = Zb[rb + kk + 2 * Q + h];
+        for (; kk + 8 <= nv; kk += 8) {
+          float a[NS][4], b[NS][4];
+          static_for<NS>([&](auto S) {
+            static_for<4>([&](auto Q) {
+              a[S][Q] = Zb[ra[S] + kk + 2 * Q + h];
+              b[S][Q] = Zb[rb[S] + kk + 2 * Q + h];
             });
-            static_for<8>([&](auto Q) { sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], sacc[S], 0, 0, 0); });
-          }
-          for (; kk < nv; kk += 2)
-            sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(Zb[ra + kk + h], Zb[rb + kk + h], sacc[S], 0, 0, 0);
+          });
+          __builtin_amdgcn_sched_barrier(0);
+          static_for<4>([&](auto Q) {
+            static_for<NS>([&](auto S) {
+              if (S + 1 < NS || lastS) sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[S][Q], b[S][Q], sacc[S], 0, 0, 0);
+            });
+          });
         }
-      });
+        for (; kk < nv; kk += 2)
+          static_for<NS>([&](auto S) {
+            if (S + 1 < NS || lastS)
+              sacc[S] = __builtin_amdgcn_mfma_f32_32x32x2f32(Zb[ra[S] + kk + h], Zb[rb[S] + kk + h], sacc[S], 0, 0, 0);
+          });
+      }
 #endif
       // S_dd tiles in register order: one coalesced 256-B row per register
       // (the final values after the chunk's last half)
