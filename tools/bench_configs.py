@@ -130,9 +130,18 @@ def main():
         k.sample_(st, -(-args.warmup // K) * K)
         nb = -(-args.steps // K)  # timed blocks of K transitions
         wall, kms = timed(lambda: k.sample_(st, K), nb, torch.cuda.current_stream(dev))
+        import bench  # the flop count and the stats-kernel timer of the N > 1 headline
+        fl = bench.pooled_flops_per_chain_step(d)
+        rate = C * nb * K / wall
+        sms = bench.pooled_stats_ms(k, st, C) / K  # transitions + chunk sums alone, per transition
         print(json.dumps({"config": f"{key} regime B" + (f", sync_every={K}" if K > 1 else ""), "chains": C,
-                          "dim": d, "steps": nb * K, "value": C * nb * K / wall, "unit": "chain-steps/s",
-                          "ms_per_step": kms / K, "mean_accept_prob": float(st.mean_accept_prob[0])}), flush=True)
+                          "dim": d, "steps": nb * K, "value": rate, "unit": "chain-steps/s",
+                          "ms_per_step": kms / K, "mean_accept_prob": float(st.mean_accept_prob[0]),
+                          "fp32": {"flops_per_chain_step": fl, "step_tflops": rate * fl / 1e12,
+                                   "step_frac": rate * fl / 1e12 / bench.FP32_PEAK_TFLOPS, "stats_ms": sms,
+                                   "stats_tflops": C * fl / (sms * 1e-3) / 1e12,
+                                   "stats_frac": C * fl / (sms * 1e-3) / 1e12 / bench.FP32_PEAK_TFLOPS,
+                                   "peak_tflops": bench.FP32_PEAK_TFLOPS}}), flush=True)
 
 
 if __name__ == "__main__":

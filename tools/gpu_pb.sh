@@ -11,4 +11,5 @@ timeout -k 10 200 python -u tools/bench_configs.py --only gauss256_pooled,pooled
 rc=$?; echo "cfg rc=$rc"; grep config gpurun_out/$TAG/cfg.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof -o run --output-format csv -- \
   python3 tools/bench_configs.py --only gauss256_pooled --steps 50 > gpurun_out/$TAG/prof.log 2>&1
-rc=$?; echo "prof rc=$rc"; exit $rc
+rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
+if [ -f adaptive-mcmc_amd/lib/diag/libamh_stamps.so ]; then timeout -k 10 120 python3 tools/upd_stamps.py --dim 256 || exit 1; fi
