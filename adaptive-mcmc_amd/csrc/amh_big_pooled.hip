@@ -773,8 +773,21 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
   const float maccn = macc + (abar - macc) / (float)n;
   const float lamn = lam + gamma * (abar - p.target);
   // (0) A = float((1-g) Sigma + g S_dd / N), formed in the 4-row-aligned
-  // layout by pooled_big_prep_kernel (all CUs): one coalesced 16-B copy
-  {
+  // layout by pooled_big_prep_kernel (all CUs): one coalesced 16-B copy.
+  // d = 64 (2,080 entries) forms it here, a wave per column, with the same
+  // double arithmetic (one launch instead of three, see (4))
+  if constexpr (NT == 2) {
+    const double g = (double)gamma;
+    for (int k = w; k < d; k += kUpdWaves) {
+      const int64_t co = col_off(d, k);
+      const int ab = a4_base(d, k);
+      if (lane < d - k) {
+        const double a = (1.0 - g) * p.in.cov[co + lane];
+        const double b = g * (sums[d + co + lane] / N);
+        A[ab + k + lane] = (float)(a + b);
+      }
+    }
+  } else {
     const int nA = d * (d + 4) / 2;
     const f32x4* src = (const f32x4*)p.scratch;
     f32x4* dst = (f32x4*)A;
@@ -901,6 +914,47 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     US(5)
   }
   const bool ok = okv != 0;
+  if constexpr (NT == 2) {
+    // d = 64: pooled_big_post_kernel's work in this block, the same float
+    // ops and sum order (a column's rows fit one wave, so of its 256-lane
+    // big_sum only the first 64-lane butterfly is non-zero)
+    __shared__ float colsum[64];
+    const double g = (double)gamma;
+    const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
+    for (int k = w; k < d; k += kUpdWaves) {
+      const int64_t co = col_off(d, k);
+      const int ab = a4_base(d, k);
+      float sq = 0.0f;
+      if (lane < d - k) {
+        const int64_t o = co + lane;
+        const float lo = p.in.scale[o];
+        const float ln = ok ? A[ab + k + lane] : lo;
+        const float tt = (ln * e1) - (lo * e0);
+        sq = tt * tt;
+        if (ok) {
+          const double a = (1.0 - g) * p.in.cov[o];
+          const double b = g * (sums[d + o] / N);
+          p.out.cov[o] = a + b;
+          p.out.scale[o] = ln;
+        } else {
+          p.out.cov[o] = p.in.cov[o];
+          p.out.scale[o] = lo;
+        }
+      }
+      const float s0 = Grp<64>::sum(sq);
+      if (lane == 0) colsum[k] = (s0 + 0.0f) + (0.0f + 0.0f);
+    }
+    __syncthreads();
+    if (w == 0) {
+      const float S = Grp<64>::sum(colsum[lane]);
+      if (lane == 0) {
+        p.out.as_change[0] = sqrtf((S + 0.0f) + (0.0f + 0.0f));
+        p.out.i[0] = itr;
+        p.out.mean_accept_prob[0] = maccn;
+        p.out.log_step_size[0] = lamn;
+      }
+    }
+  } else {
   // (4) the new factor back to the staging buffer (coalesced) with the ok
   // flag, gamma and e^lam, e^lam' for pooled_big_post_kernel (all CUs), which
   // copies it to out.scale / out.cov and forms the as_change terms
@@ -918,6 +972,7 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
       p.out.mean_accept_prob[0] = maccn;
       p.out.log_step_size[0] = lamn;
     }
+  }
   }
   if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
   US(4)
@@ -1070,7 +1125,8 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, bool sigma_ready) {
   const size_t shm = (size_t)p.d * (p.d + 4) / 2 * sizeof(float);
   hipError_t e = hipSuccess;
-  if (!sigma_ready) {  // else pooled_final_kernel formed Sigma' already
+  const bool in_block = p.d == 64;  // d = 64: prep and post run inside the update block
+  if (!sigma_ready && !in_block) {  // else pooled_final_kernel formed Sigma' already
     hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1094,6 +1150,7 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, boo
   }
   e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (in_block) return hipSuccess;
   hipLaunchKernelGGL(pooled_big_post_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
   return hipGetLastError();
 }
