@@ -902,6 +902,12 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     const uint32_t la = wb_a + (uint32_t)r * 4u;  // this lane's dword in the factor region
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): item k has landed
+#ifndef AMH_S64_NOPRIO
+    // the hand-over phase (stores, LDS -> registers, the next DMA) at high
+    // wave priority so the memory queue is re-armed before other waves'
+    // compute: 239 -> 236 us per launch (tools/gpu_prio.sh A/B)
+    __builtin_amdgcn_s_setprio(3);
+#endif
     // ---- item k-1's z / loc / scalars leave from registers
     if (prev >= 0) store_small(prev, r);
     const bool wr = prev >= 0 && prev_upd;
@@ -963,6 +969,9 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       prefetch_item<64, false>(p, nxt, D, wb, lane);
       nxt2 = ticket();
     }
+#ifndef AMH_S64_NOPRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
 
     nacc = 0;
     bool updated = false;
