@@ -10,6 +10,6 @@ rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|Error" gpurun_out/$TAG/pytes
 timeout -k 10 200 python -u tools/bench_configs.py --only gauss256_pooled,pooled64 --steps 50 > gpurun_out/$TAG/cfg.log 2>&1
 rc=$?; echo "cfg rc=$rc"; grep config gpurun_out/$TAG/cfg.log; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/$TAG/prof -o run --output-format csv -- \
-  python3 tools/bench_configs.py --only gauss256_pooled --steps 50 > gpurun_out/$TAG/prof.log 2>&1
+  python3 tools/bench_configs.py --only gauss256_pooled,pooled64 --steps 50 > gpurun_out/$TAG/prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 if [ -f adaptive-mcmc_amd/lib/diag/libamh_stamps.so ]; then timeout -k 10 120 python3 tools/upd_stamps.py --dim 256 || exit 1; fi
