@@ -579,11 +579,22 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
       }
       __syncthreads();
       // (6) the chunk's sums: S_d, S_a sequential over chains, S_dd on MFMA
+      // sequential adds in chain order, the LDS reads batched 16 at a time
+      // (the slots past nv hold +0, and adding +0 to a sum that started at
+      // +0 changes no bit, so all 64 are added)
       if (tid < D) {
-        for (int c = 0; c < nv; ++c) sd = sd + Zb[tid * kLd + c];
+        static_for<4>([&](auto B) {
+          float x[16];
+          static_for<16>([&](auto Q) { x[Q] = Zb[tid * kLd + 16 * B + Q]; });
+          static_for<16>([&](auto Q) { sd = sd + x[Q]; });
+        });
       }
       if (tid == 64 * kFBWaves - 1) {
-        for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+        static_for<4>([&](auto B) {
+          float x[16];
+          static_for<16>([&](auto Q) { x[Q] = alph[16 * B + Q]; });
+          static_for<16>([&](auto Q) { sa = sa + x[Q]; });
+        });
       }
       cnt += nv;
       {
