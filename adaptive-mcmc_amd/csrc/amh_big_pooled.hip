@@ -199,14 +199,24 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   __syncthreads();
   // (6) the chunk's sums: S_d, S_a sequential over chains, S_dd on MFMA
   double* out = p.partials + chunk * V;
+  // sequential adds in chain order, LDS reads batched 16 at a time (slots
+  // past nv hold +0: adding +0 to a sum that started at +0 changes no bit)
   if (tid < d) {
     float sd = 0.0f;
-    for (int c = 0; c < nv; ++c) sd = sd + Zb[tid * kFLd + c];
+    static_for<4>([&](auto B) {
+      float x[16];
+      static_for<16>([&](auto Q) { x[Q] = Zb[tid * kFLd + 16 * B + Q]; });
+      static_for<16>([&](auto Q) { sd = sd + x[Q]; });
+    });
     out[tid] = (double)sd;
   }
   if (tid == 64) {
     float sa = 0.0f;
-    for (int c = 0; c < nv; ++c) sa = sa + alph[c];
+    static_for<4>([&](auto B) {
+      float x[16];
+      static_for<16>([&](auto Q) { x[Q] = alph[16 * B + Q]; });
+      static_for<16>([&](auto Q) { sa = sa + x[Q]; });
+    });
     out[d + P] = (double)sa;
     out[d + P + 1] = (double)nv;
   }
