@@ -257,3 +257,38 @@ def test_pooled_noise_ahead_invalidation(d, C, gpu, orc):
         assert st.z.cpu().numpy().tobytes() == z.tobytes(), f"z differs at step {t + 1}"
         assert st.adapt_state.scale.cpu().numpy().tobytes() == np.asarray(sh["L"]).tobytes(), f"L at step {t + 1}"
         assert st.as_change.cpu().numpy().tobytes() == np.asarray(sh["asc"]).astype(np.float32).tobytes()
+
+
+@pytest.mark.parametrize("d,C", [(64, 500), (128, 300)])
+def test_pooled_keep_factor_when_not_pd(d, C, gpu, orc):
+    """The update's keep-L branch (arwmh.py:191) through the large-d path:
+    after two steps the shared covariance is replaced by a negative one, so
+    Sigma' is not positive definite and the factor and covariance are kept;
+    as_change, mu, lambda still move.  d = 64 runs the update's in-block
+    prep / post, d = 128 the all-CU prep / post kernels with the
+    last-arriver as_change sum.  Bit for bit against the oracle."""
+    from kernels_amd import PooledARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", d)
+    k = PooledARWMH(num_chains=C, **kw)
+    z0 = np.random.default_rng(5).uniform(-2, 2, size=(C, d)).astype(np.float32)
+    st = k.init(PRNGKey(5), 0, torch.as_tensor(z0), (), mk)
+    ost = orc.init(om, PRNGKey(5), C, init_z=z0)
+    z, pe, keys = ost.z, ost.potential_energy, ost.rng_key
+    sh = orc.pooled_init_shared(d)
+    for t in range(4):
+        if t == 2:
+            neg = -1000.0 * np.asarray(sh["cov"])
+            st.cov.copy_(torch.as_tensor(neg))
+            sh["cov"] = neg.copy()
+        L_before = np.asarray(sh["L"]).copy()
+        st = k.sample(st)
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]))
+        orc.pooled_update(om, sums, sh)
+        torch.cuda.synchronize()
+        if t == 2:
+            assert np.array_equal(np.asarray(sh["L"]), L_before), "oracle did not keep the factor"
+        for name, a, b in (("z", st.z, z), ("L", st.adapt_state.scale, sh["L"]), ("cov", st.cov, sh["cov"]),
+                           ("mu", st.adapt_state.loc, sh["mu"]), ("asc", st.as_change, sh["asc"]),
+                           ("lam", st.adapt_state.log_step_size, sh["lam"])):
+            a = a.cpu().numpy()
+            assert a.tobytes() == np.asarray(b).astype(a.dtype).tobytes(), f"{name} differs at step {t + 1}"
