@@ -173,28 +173,37 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
                                    std::to_string(h->cfg.dim));
   if (dm > 64 && !amh::big_model(model_id, dm))
     return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model with d a multiple of 32 (<= 256)");
-  h->model_id = model_id;
-  h->model.data = data;
-  const bool dia = model_id == AMH_MODEL_DIAMONDS || model_id == AMH_MODEL_DIAMONDS_SS;
-  h->model.n = (model_id == AMH_MODEL_KIDIQ || dia) ? iparams[0] : 0;
-  h->model.k = dia ? iparams[1] : 0;
-  h->n_data = n_data;
+  // the handle's device for everything below (the caller -- Handle.bind_model --
+  // holds it current and restores its own afterwards)
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_bind_model/hipSetDevice");
   if (h->xpack) {
     (void)hipDeviceSynchronize();  // a queued launch may still read the old copy
     (void)hipFree(h->xpack);
     h->xpack = nullptr;
   }
+  h->model_id = 0;  // unbound until the whole binding has succeeded
+  h->model.data = data;
+  const bool dia = model_id == AMH_MODEL_DIAMONDS || model_id == AMH_MODEL_DIAMONDS_SS;
+  h->model.n = (model_id == AMH_MODEL_KIDIQ || dia) ? iparams[0] : 0;
+  h->model.k = dia ? iparams[1] : 0;
+  h->n_data = n_data;
   if (model_id == AMH_MODEL_DIAMONDS && amh::split_model(model_id, dm)) {
-    // the MFMA potential's tile copy of Xc and Y, made once here (synchronous)
+    // the MFMA potential's tile copy of Xc and Y, made once here (synchronous,
+    // on the null stream: the caller has synchronised the stream that wrote data)
     const int64_t nf = amh::diamonds_pack_floats(h->model.n, h->model.k);
     if (nf > 0) {
-      hipError_t e = hipSetDevice(h->device);
-      if (e == hipSuccess) e = hipMalloc(&h->xpack, (size_t)nf * sizeof(float));
+      e = hipMalloc(&h->xpack, (size_t)nf * sizeof(float));
       if (e == hipSuccess) e = amh::run_diamonds_pack(h->model, h->xpack, nullptr);
       if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-      if (e != hipSuccess) return hip_fail(h, e, "amh_bind_model(diamonds tile copy)");
+      if (e != hipSuccess) {
+        if (h->xpack) (void)hipFree(h->xpack);
+        h->xpack = nullptr;
+        return hip_fail(h, e, "amh_bind_model(diamonds tile copy)");
+      }
     }
   }
+  h->model_id = model_id;
   return AMH_OK;
 }
 

@@ -304,9 +304,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     const bool chain_ok = chain < C;
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this item's DMA has landed
-#ifndef AMH_STEP_NOPRIO
     __builtin_amdgcn_s_setprio(3);  // hand-over phase first (as arwmh_step64_kernel): diamonds_ss +1.8 %
-#endif
     AMH_STAMP(0)
     if (prev >= 0) store_item(prev, lane);
     AMH_STAMP(1)
@@ -349,23 +347,16 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       prefetch_item<G, kExt>(p, nxt * CPW, d, wb, lane);
       nxt2 = ticket();
     }
-#ifndef AMH_STEP_NOPRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
     AMH_STAMP(3)
 
     nacc = 0;
     updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
-#ifndef AMH_ABLATE_RNG
       const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
       const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
       const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
-#else
-      const float xi = act ? (float)((r * 7 + it) % 13) * 0.1f - 0.6f : 0.0f;
-      const float u = (float)(it % 10) * 0.1f;
-#endif
 
       // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
       //      L xi = U (dl * xi)
@@ -382,16 +373,12 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
 
       // ---- potential, NaN -> +inf (arwmh.py:169-171)
-#ifndef AMH_ABLATE_POT
       float pep;
       if constexpr (kExt) {
         pep = pe_ext;  // n_steps == 1 (host-enforced)
       } else {
         pep = M<G>::potential(zp, r, d, mctx, lds);
       }
-#else
-      float pep = Gp::sum(zp * zp);
-#endif
       if (amh_isnan(pep)) pep = INFINITY;
 
       // ---- accept / reject (arwmh.py:173-178)
@@ -424,7 +411,6 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       // sweep 1: w*_j = w_j when column j is applied (forward solve U w* = delta)
       float w = delta;
       float ws = 0.0f;
-#ifndef AMH_ABLATE_SWEEP1
       static_for<DMAX>([&](auto J) {
         if (J < d) {
           const float wj = Gp::template bcast<J>(w);
@@ -433,9 +419,6 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         }
         column_fence<J>();
       });
-#else
-      ws = w * U[3];
-#endif
 
       // per-column scalars, one column per lane; b_j by exclusive scan
       const float gw2 = act ? gamma * (ws * ws) : 0.0f;
@@ -452,11 +435,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       // per-column quantities, and every off-diagonal entry is finite whenever
       // they are ("keep-L rule").  So the keep-L test of
       // arwmh.py:191 is decided before the factor is touched.
-#ifndef AMH_ABLATE_SWEEP2
       const bool revert = Gp::any(act && amh_isnan(dnew));
-#else
-      const bool revert = Gp::any(act && amh_isnan(dnew)) || true;
-#endif
       float sacc = 0.0f;
       float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};  // as_change partial sums (columns j mod 4)
       if (!revert) {
@@ -730,31 +709,26 @@ static_assert(kS64Z == 2080 && kS64S == kS64M + 64, "layout of prefetch_item<64>
 constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)kS64Waves * kS64WB + 32) * sizeof(float); }
 
 constexpr int s64_col(int j) { return j * 64 - j * (j - 1) / 2; }  // packed column offset
-#ifdef AMH_S64_NOP
-#define S64_NOP "s_nop 4\n\t"
-#else
-#define S64_NOP ""
-#endif
 
 // lanes r > J read the dword at a + OFF into x (others keep x); pending until lds_wait
 template <int J, int OFF>
 __device__ __forceinline__ void s64_rd_above(float& x, uint32_t a) {
   uint64_t sv;
-  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %3\n\t" S64_NOP "ds_read_b32 %0, %2 offset:%4\n\t" S64_NOP "s_mov_b64 exec, %1"
+  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %3\n\tds_read_b32 %0, %2 offset:%4\n\ts_mov_b64 exec, %1"
                : "+v"(x), "=&s"(sv) : "v"(a), "n"(J + 1), "n"(OFF));
 }
 // lanes r >= J write v to a + OFF
 template <int J, int OFF>
 __device__ __forceinline__ void s64_wr_from(uint32_t a, float v) {
   uint64_t sv;
-  asm volatile("s_mov_b64 %0, exec\n\ts_lshl_b64 exec, -1, %3\n\t" S64_NOP "ds_write_b32 %1, %2 offset:%4\n\t" S64_NOP "s_mov_b64 exec, %0"
+  asm volatile("s_mov_b64 %0, exec\n\ts_lshl_b64 exec, -1, %3\n\tds_write_b32 %1, %2 offset:%4\n\ts_mov_b64 exec, %0"
                : "=&s"(sv) : "v"(a), "v"(v), "n"(J), "n"(OFF) : "memory");
 }
 // lanes r > J: u = t * s
 template <int J>
 __device__ __forceinline__ void s64_mul_above(float& u, float t, float s) {
   uint64_t sv;
-  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %4\n\t" S64_NOP "v_mul_f32 %0, %2, %3\n\t" S64_NOP "s_mov_b64 exec, %1"
+  asm volatile("s_mov_b64 %1, exec\n\ts_lshl_b64 exec, -1, %4\n\tv_mul_f32 %0, %2, %3\n\ts_mov_b64 exec, %1"
                : "+v"(u), "=&s"(sv) : "v"(t), "v"(s), "n"(J + 1));
 }
 // sweep 1, column J: w_J broadcast, then w -= w_J U_rJ on lanes r > J.  A VALU
@@ -873,18 +847,6 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   auto flush_factor = [&](int64_t c) {
     const Buf Lout(uniform_ptr(p.out.scale + c * P), P * 4u);
     const uint32_t la = wb_a + (uint32_t)lane_id() * 16u;
-#ifdef AMH_S64_FLUSH9
-    f32x4 v[9];
-    v[0] = lds_ld4<0>(la); v[1] = lds_ld4<1024>(la); v[2] = lds_ld4<2048>(la);
-    v[3] = lds_ld4<3072>(la); v[4] = lds_ld4<4096>(la); v[5] = lds_ld4<5120>(la);
-    v[6] = lds_ld4<6144>(la); v[7] = lds_ld4<7168>(la); v[8] = lds_ld4<8192>(la);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]),
-                 "+v"(v[6]), "+v"(v[7]), "+v"(v[8]));
-    static_for<9>([&](auto Q) {
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uint32x4_t_, v[(int)Q]), Lout.rs,
-                                             (int)(1024u * Q + 16u * (uint32_t)lane_id()), 0, AMH_STORE_AUX);
-    });
-#else
     static_for<3>([&](auto G) {  // three dwordx4 per lane in flight per wait
       f32x4 v[3];
       static_for<3>([&](auto Q) { v[(int)Q] = lds_ld4<1024 * (3 * G + Q)>(la); });
@@ -895,7 +857,6 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
                                                AMH_STORE_AUX);
       });
     });
-#endif
   };
 
   int64_t item = ticket();
@@ -908,12 +869,10 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     const uint32_t la = wb_a + (uint32_t)r * 4u;  // this lane's dword in the factor region
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): item k has landed
-#ifndef AMH_S64_NOPRIO
     // the hand-over phase (stores, LDS -> registers, the next DMA) at high
     // wave priority so the memory queue is re-armed before other waves'
     // compute: 239 -> 236 us per launch (tools/gpu_prio.sh A/B)
     __builtin_amdgcn_s_setprio(3);
-#endif
     // ---- item k-1's z / loc / scalars leave from registers
     if (prev >= 0) store_small(prev, r);
     const bool wr = prev >= 0 && prev_upd;
@@ -975,9 +934,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       prefetch_item<64, false>(p, nxt, D, wb, lane);
       nxt2 = ticket();
     }
-#ifndef AMH_S64_NOPRIO
     __builtin_amdgcn_s_setprio(0);
-#endif
 
     nacc = 0;
     bool updated = false;
@@ -990,23 +947,17 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167), L xi = U (dl * xi)
       const float el = amh_expf(lam);
       const float eta = dl * xi;
-#ifndef AMH_S64_BC_RL
       s64_wr(x_a + (uint32_t)r * 4u, eta);
-#endif
       float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
       static_for<D / kS64EB>([&](auto B) {  // kS64EB columns per batch
         constexpr int b = B;
         f32x4 e[kS64EB / 4];
-#ifndef AMH_S64_BC_RL
         static_for<kS64EB / 4>([&](auto Q) { e[(int)Q] = lds_ld4<16 * (kS64EB / 4 * b + Q)>(x_a); });
         if constexpr (kS64EB == 16) {
           lds_wait(e[0], e[1], e[2], e[3]);
         } else {
           s64_tie(e[0], e[1]);
         }
-#else
-        static_for<kS64EB>([&](auto K) { e[(int)K / 4][(int)K % 4] = Gp::template bcast<kS64EB * b + K>(eta); });
-#endif
         static_for<kS64EB>([&](auto K) {
           constexpr int j = kS64EB * b + K;
           a4[j & 3] = fmaf(U[j], e[(int)K / 4][(int)K % 4], a4[j & 3]);
@@ -1020,9 +971,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       float pep;
       {
         const float diff = zp - mctx.mr;
-#ifndef AMH_S64_BC_RL
         s64_wr(x_a + (uint32_t)r * 4u, diff);
-#endif
         f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
         static_for<D / kS64PB>([&](auto B) {
           constexpr int b = B;
@@ -1030,11 +979,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
           f32x4 pv[NQ], dv[NQ];
           static_for<NQ>([&](auto Q) {
             pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
-#ifndef AMH_S64_BC_RL
             dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
-#else
-            static_for<4>([&](auto K) { dv[(int)Q][(int)K] = Gp::template bcast<kS64PB * b + 4 * Q + K>(diff); });
-#endif
           });
           if constexpr (NQ == 4) {
             asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
@@ -1088,24 +1033,11 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
 
       // sweep 1 (lanes r > j): afterwards lane r holds w*_r (forward solve U w* = delta)
-#ifndef AMH_S64_SW1_OLD
       float ws = delta;
       static_for<D - 1>([&](auto J) {
         s64_sweep1<J>(ws, U[J]);
         column_fence<J>();
       });
-#else
-      float ws = 0.0f;
-      {
-        float w = delta;
-        static_for<D>([&](auto J) {
-          const float wj = Gp::template bcast<J>(w);
-          ws = capture<64, J>(ws, wj, r);
-          w = fmaf(-wj, U[J], w);
-          column_fence<J>();
-        });
-      }
-#endif
 
       const float gw2 = gamma * (ws * ws);
       const float tsc = gw2 / Dg;
@@ -1125,22 +1057,12 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
         float w = delta;
         static_for<16>([&](auto G4) {
           constexpr int g = G4;
-#ifndef AMH_S64_BC_RL
           // the four coefficient vectors of columns 16(g/4) .. +15 (lanes of that quarter write)
           if constexpr (g % 4 == 0) s64_wr4_quarter<g / 4>(xq_a, ws, c, ac, bc);
           constexpr int gq = g % 4;
           f32x4 cw = lds_ld4<16 * gq>(x_a), cc = lds_ld4<64 + 16 * gq>(x_a);
           f32x4 ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
           lds_wait(cw, cc, ca, cb);
-#else
-          f32x4 cw, cc, ca, cb;
-          static_for<4>([&](auto Q) {
-            cw[(int)Q] = Gp::template bcast<4 * g + Q>(ws);
-            cc[(int)Q] = Gp::template bcast<4 * g + Q>(c);
-            ca[(int)Q] = Gp::template bcast<4 * g + Q>(ac);
-            cb[(int)Q] = Gp::template bcast<4 * g + Q>(bc);
-          });
-#endif
           static_for<4>([&](auto Q) {
             constexpr int j = 4 * g + Q;
             const float uo = U[j];

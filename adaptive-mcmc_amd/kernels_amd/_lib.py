@@ -49,6 +49,11 @@ class AmhCollect(ctypes.Structure):
                 ("thinning", ctypes.c_int32)]
 
 
+class AmhPooledState(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in ("i", "z", "potential_energy", "rng_key", "mean_accept_prob", "loc",
+                                               "scale", "log_step_size", "as_change", "cov")]
+
+
 class AmhError(RuntimeError):
     pass
 
@@ -100,6 +105,18 @@ def lib():
     L.amh_normals.restype = ctypes.c_int
     L.amh_sinkhorn_lse.argtypes = [P, I64, I64, P, F, F, P, P]
     L.amh_sinkhorn_lse.restype = ctypes.c_int
+    PS = ctypes.POINTER(AmhPooledState)
+    L.amh_pooled_sums_size.argtypes = [I32, ctypes.POINTER(I64)]
+    L.amh_pooled_stats.argtypes = [P, I64, PS, P, P, P, P]
+    L.amh_pooled_update.argtypes = [P, P, PS, PS, P]
+    L.amh_pooled_step.argtypes = [P, I64, PS, PS, I32, P, P]
+    L.amh_pooled_stats_k.argtypes = [P, I64, PS, I32, P, P, P, P]
+    L.amh_pooled_update_k.argtypes = [P, P, PS, PS, I32, P]
+    L.amh_pooled_step_k.argtypes = [P, I64, PS, PS, I32, I32, P, P]
+    for name in ("amh_pooled_sums_size", "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step",
+                 "amh_pooled_stats_k", "amh_pooled_update_k", "amh_pooled_step_k"):
+        getattr(L, name).restype = ctypes.c_int
+    L.amh_version.argtypes = []
     for name in EXPORTS[:10]:
         getattr(L, name).restype = ctypes.c_int if name != "amh_last_error" else ctypes.c_char_p
     _lib = L
@@ -148,7 +165,11 @@ class Handle:
     def bind_model(self, model_id: int, data: torch.Tensor, iparams=()):
         require_gpu(data)
         ip = (ctypes.c_int64 * max(1, len(iparams)))(*iparams)
-        check(self._lib.amh_bind_model(self.h, model_id, ptr(data), data.numel(), ip, len(iparams)), self.h)
+        with torch.cuda.device(self.device):
+            # the library may copy `data` on the null stream: let the stream
+            # that produced it finish first
+            torch.cuda.current_stream(data.device).synchronize()
+            check(self._lib.amh_bind_model(self.h, model_id, ptr(data), data.numel(), ip, len(iparams)), self.h)
         self._data = data  # keep alive
 
     def close(self):

@@ -17,6 +17,7 @@ torch.distributed (RCCL over xGMI on MI355X).
 from __future__ import annotations
 
 import ctypes
+import weakref
 from collections import namedtuple
 
 import torch
@@ -31,28 +32,7 @@ PooledState = namedtuple("PooledState", ["i", "z", "potential_energy", "mean_acc
 PooledAdaptState = namedtuple("PooledAdaptState", ["loc", "scale", "log_step_size"])
 
 
-class AmhPooledState(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in ("i", "z", "potential_energy", "rng_key", "mean_accept_prob", "loc",
-                                               "scale", "log_step_size", "as_change", "cov")]
-
-
-def _bind_pooled(L):
-    if getattr(L, "_pooled_bound", False):
-        return L
-    P, I32, I64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64
-    PS = ctypes.POINTER(AmhPooledState)
-    L.amh_pooled_sums_size.argtypes = [I32, ctypes.POINTER(I64)]
-    L.amh_pooled_stats.argtypes = [P, I64, PS, P, P, P, P]
-    L.amh_pooled_update.argtypes = [P, P, PS, PS, P]
-    L.amh_pooled_step.argtypes = [P, I64, PS, PS, I32, P, P]
-    L.amh_pooled_stats_k.argtypes = [P, I64, PS, I32, P, P, P]
-    L.amh_pooled_update_k.argtypes = [P, P, PS, PS, I32, P]
-    L.amh_pooled_step_k.argtypes = [P, I64, PS, PS, I32, I32, P, P]
-    for n in ("amh_pooled_sums_size", "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step",
-              "amh_pooled_stats_k", "amh_pooled_update_k", "amh_pooled_step_k"):
-        getattr(L, n).restype = ctypes.c_int
-    L._pooled_bound = True
-    return L
+AmhPooledState = _lib.AmhPooledState
 
 
 def sums_size(d: int) -> int:
@@ -104,6 +84,7 @@ class PooledARWMH(ARWMH):
         self._sums = None
         self._bufs = None
         self._pending = None  # overlap: (buffer index, all-reduce event or None) not yet applied
+        self._last_out = None  # overlap: weak reference to the z leaf of the state the pending sums belong to
         self._comm = None
         self.sync_every = int(sync_every)
         self.overlap = bool(overlap)
@@ -129,6 +110,7 @@ class PooledARWMH(ARWMH):
         self._bufs = torch.zeros(2, sums_size(d), dtype=torch.float64, device=dev)
         self._sums = self._bufs[0]
         self._pending = None
+        self._last_out = None
         return PooledState(torch.zeros(1, dtype=torch.int32, device=dev), st.z, st.potential_energy,
                            torch.zeros(1, **f), adapt, torch.zeros(1, **f), st.rng_key, cov)
 
@@ -195,7 +177,7 @@ class PooledARWMH(ARWMH):
                                          self.sync_every, _lib.stream_ptr(dev)), self._handle.h)
 
     def _one(self, sin: PooledState, sout: PooledState):
-        L = _bind_pooled(_lib.lib())
+        L = _lib.lib()
         dev = sin.z.device.index
         C = sin.z.shape[0]
         cin, cout = self._c(sin), self._c(sout)
@@ -209,6 +191,13 @@ class PooledARWMH(ARWMH):
                 self._update(L, buf, cin, cout)
                 self._sums = buf
                 return
+            last = self._last_out() if self._last_out is not None else None
+            if self._pending is not None and last is not sin.z:
+                # a state this sampler did not just produce: the pending sums
+                # belong to another trajectory, so this block starts afresh
+                # (theta_1 = theta_0).  A checkpoint carries them instead
+                # (checkpoint.state_dict(state, kernel)).
+                self._pending = None
             b = 0 if self._pending is None else 1 - self._pending[0]
             buf = self._bufs[b]
             self._stats(L, cin, sout, buf, C)
@@ -228,7 +217,32 @@ class PooledARWMH(ARWMH):
                         c.copy_(a)
                 torch.add(sin.i, self.sync_every, out=sout.i)
             self._pending = (b, ev)
+            self._last_out = weakref.ref(sout.z)
             self._sums = buf
+
+    # ------------------------------------------------ checkpoint (overlap) --
+    def pending_sums(self):
+        """overlap = True: the all-reduced sums of the last block, not yet
+        applied (they update the shared state at the start of the next block),
+        as a host float64 array; None when nothing is pending."""
+        if self._pending is None:
+            return None
+        b, ev = self._pending
+        if ev is not None:
+            ev.synchronize()
+        torch.cuda.synchronize(self._bufs.device)
+        return self._bufs[b].detach().cpu().numpy().copy()
+
+    def set_pending_sums(self, state, sums):
+        """Make `sums` the pending sums of `state` (resume of an overlap run:
+        the next block applies them exactly as the uninterrupted run would)."""
+        if not self.overlap:
+            raise ValueError("pending sums exist only with overlap=True")
+        if self._bufs is None:
+            raise RuntimeError("call init() first")
+        self._bufs[0].copy_(torch.as_tensor(sums, dtype=torch.float64))
+        self._pending = (0, None)
+        self._last_out = weakref.ref(state.z)
 
     def sample(self, state, model_args=(), model_kwargs=None):
         """One pooled transition of every chain (sync_every > 1: one block of
@@ -245,7 +259,7 @@ class PooledARWMH(ARWMH):
         if int(n_steps) % K != 0:
             raise ValueError(f"n_steps ({n_steps}) must be a multiple of sync_every ({K})")
         if self._world() == 1 and not self.overlap:
-            L = _bind_pooled(_lib.lib())
+            L = _lib.lib()
             dev = state.z.device.index
             c = self._c(state)
             with torch.cuda.device(dev):
@@ -271,6 +285,8 @@ class PooledARWMH(ARWMH):
                        (out.mean_accept_prob, state.mean_accept_prob), (out.as_change, state.as_change),
                        (out.cov, state.cov)) + tuple(zip(out.adapt_state, state.adapt_state)):
             t.copy_(src)
+        if self._last_out is not None and self._last_out() is state.z:
+            self._last_out = weakref.ref(out.z)  # the pending sums continue with the copy
         keep = int(n_steps) // int(thinning)
         dev = state.z.device
         cz = torch.empty(keep, C, self._dim, dtype=torch.float32, device=dev) if collect_z and keep else None

@@ -115,6 +115,17 @@ def _lse_half(cost: torch.Tensor, pot: torch.Tensor, log_w: float, eps: float) -
     return out
 
 
+def _cost_mode(cost_fn) -> str:
+    """'euclidean' / 'sqeuclidean' from a name, or from an ott cost object
+    (`costs.Euclidean()`, the reference's default at evaluation.py:69, or
+    `costs.SqEuclidean()`) by its class name."""
+    name = cost_fn if isinstance(cost_fn, str) else type(cost_fn).__name__
+    key = name.lower()
+    if key in ("euclidean", "sqeuclidean"):
+        return key
+    raise ValueError(f"cost_fn must be 'euclidean' / 'sqeuclidean' or an ott Euclidean / SqEuclidean cost, got {cost_fn!r}")
+
+
 def sinkhorn(u_values, v_values, cost_fn="euclidean", epsilon=None, threshold=1e-3, max_iterations=2000,
              inner_iterations=10, relative_epsilon="std"):
     """Log-domain Sinkhorn between the uniform empirical measures of u (n, d)
@@ -123,15 +134,19 @@ def sinkhorn(u_values, v_values, cost_fn="euclidean", epsilon=None, threshold=1e
     then h <- -eps LSE_i((f_i - C_ij)/eps + log a); the column-marginal error
     sum_j b |exp((g_j - h_j)/eps) - 1| is checked every `inner_iterations`
     iterations before g <- h.  The cost matrix is materialised once (and its
-    transpose for the column half)."""
+    transpose for the column half).
+
+    The default epsilon is 0.05 x the standard deviation of the cost matrix
+    (ott's `relative_epsilon="std"` of newer releases); older ott releases
+    scaled by the mean (`relative_epsilon="mean"` here).  The reference pins no
+    ott version, so which one it saw is unpinned."""
     x, y = _dev(u_values), _dev(v_values)
     if x.shape[1] != y.shape[1]:
         raise ValueError("u_values and v_values need the same dimension")
     C = _dist2(x, y)
-    if cost_fn in ("euclidean", "Euclidean"):
+    mode = _cost_mode(cost_fn)
+    if mode == "euclidean":
         C = C.clamp_(min=0.0).sqrt_()
-    elif cost_fn not in ("sqeuclidean", "SqEuclidean"):
-        raise ValueError(f"cost_fn must be 'euclidean' or 'sqeuclidean', got {cost_fn!r}")
     if epsilon is None:
         scale = C.double().std(correction=0) if relative_epsilon == "std" else C.double().mean()
         epsilon = 0.05 * float(scale)

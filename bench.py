@@ -260,8 +260,7 @@ def pooled_stats_ms(k, st, C, reps=20):
     import ctypes
     import torch
     from kernels_amd import _lib
-    from kernels_amd.pooled import _bind_pooled
-    L = _bind_pooled(_lib.lib())
+    L = _lib.lib()
     dev = st.z.device.index
     c = k._c(st)
     zt, pt = torch.empty_like(st.z), torch.empty_like(st.potential_energy)

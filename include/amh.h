@@ -5,7 +5,7 @@
  * The reference (savelovme/adaptive-mcmc) has no FFI: its boundary is the
  * NumPyro MCMCKernel object python/kernels/arwmh.py:31.  Each entry point
  * below replaces one method of that object for a whole batch of chains; the
- * Python mirror (adaptive-mcmc_amd/kernels/arwmh.py) binds them with ctypes.
+ * Python mirror (adaptive-mcmc_amd/kernels_amd/arwmh.py, _lib.py) binds them with ctypes.
  *
  *   amh_create / amh_bind_model   ARWMH.__init__        arwmh.py:43-78
  *                                 + model plug-in        arwmh.py:109-116

@@ -38,6 +38,30 @@ def test_library_exports_every_declared_symbol(lib):
     assert sorted(lib.EXPORTS) == header_symbols()
 
 
+def header_arity():
+    """{symbol: parameter count} from the prototypes in include/amh.h."""
+    src = open(os.path.join(ROOT, "include", "amh.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    out = {}
+    for m in re.finditer(r"^\s*(?:int64_t|int|const char\s*\*)\s*(amh_\w+)\s*\(([^;]*?)\)\s*;", src, flags=re.M | re.S):
+        params = " ".join(m.group(2).split())
+        out[m.group(1)] = 0 if params in ("", "void") else params.count(",") + 1
+    return out
+
+
+def test_binding_arity_matches_header(lib):
+    """Every ctypes binding declares exactly as many argtypes as the header's
+    prototype has parameters (amh_pooled_stats_k was bound with
+    7 of its 8)."""
+    ar = header_arity()
+    assert sorted(ar) == header_symbols()
+    L = lib.lib()
+    for s, n in ar.items():
+        at = getattr(L, s).argtypes
+        assert at is not None, f"{s}: no argtypes bound"
+        assert len(at) == n, f"{s}: binding has {len(at)} argtypes, amh.h declares {n} parameters"
+
+
 def test_version(lib):
     assert lib.lib().amh_version() == 1
 

@@ -31,6 +31,26 @@ def test_roundtrip(kind, tmp_path):
         assert torch.equal(a, b)
 
 
+def test_path_suffix_and_extras(tmp_path):
+    """save_state appends ".npz" as np.savez does and load_state finds it;
+    extra arrays come back with with_extras=True."""
+    import kernels_amd as K
+    st = K.ARWMHState(torch.zeros(3, dtype=torch.int32), torch.ones(3, 2), torch.zeros(3), torch.zeros(3),
+                      K.ARWMHAdaptState(torch.zeros(3, 2), torch.ones(3, 3), torch.zeros(3)), torch.zeros(3),
+                      torch.zeros(3, 2, dtype=torch.int32))
+    p = K.save_state(str(tmp_path / "run"), st, accept_count=torch.arange(3, dtype=torch.int32))
+    assert p.endswith("run.npz")
+    back, extra = K.load_state(str(tmp_path / "run"), "cpu", with_extras=True)
+    assert torch.equal(back.z, st.z) and list(extra) == ["accept_count"]
+    assert np.array_equal(extra["accept_count"], np.arange(3))
+    with pytest.raises(ValueError):
+        K.save_state(str(tmp_path / "x"), st, z=torch.zeros(1))
+    sd = K.state_dict(st)
+    sd["__pooled_pending_sums__"] = np.zeros(4)
+    with pytest.raises(ValueError):
+        K.load_state_dict(sd, "cpu")  # pending pooled sums need the continuing kernel
+
+
 def test_rejects_unknown():
     import kernels_amd as K
     with pytest.raises(TypeError):

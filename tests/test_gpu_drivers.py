@@ -62,34 +62,44 @@ def test_collect_states_logscale_eight_schools_golden(gpu):
             assert np.max(np.abs(S1 - Sg)) <= 1e-3 * np.max(np.abs(Sg)) + 1e-5, (int(t), c)
 
 
-@pytest.mark.parametrize("kind,d", [("arwmh", 64), ("arwmh", 256), ("asss", 12), ("pooled", 128)])
+@pytest.mark.parametrize("kind,d", [("arwmh", 64), ("arwmh", 256), ("asss", 12), ("pooled", 128),
+                                    ("pooled_overlap", 64), ("pooled_overlap", 128)])
 def test_checkpoint_resume_is_exact(kind, d, gpu, tmp_path):
     """SURVEY.md §5 checkpoint / resume: save the state after 7 transitions,
     load it into a fresh kernel of the same configuration and continue for 5;
     the result equals 12 uninterrupted transitions bit for bit (the step is a
-    pure function of the state; d = 256 also crosses the chained proposal)."""
+    pure function of the state; d = 256 also crosses the chained proposal).
+    With overlap=True the sums pending in the sampler travel in the
+    checkpoint and are handed to the fresh kernel."""
     import posteriors as P
     from kernels_amd import ARWMH, ASSS, PRNGKey, PooledARWMH, load_state, save_state
-    cls = {"arwmh": ARWMH, "asss": ASSS, "pooled": PooledARWMH}[kind]
+    cls = {"arwmh": ARWMH, "asss": ASSS, "pooled": PooledARWMH, "pooled_overlap": PooledARWMH}[kind]
+    kw = dict(overlap=True) if kind == "pooled_overlap" else {}
+    pooled = kind.startswith("pooled")
     C = 300
     z0 = torch.empty(C, d, device=gpu).uniform_(-2, 2)
 
     def fresh():
-        k = cls(potential_fn=P.correlated_gaussian(d), num_chains=C, device=gpu)
+        k = cls(potential_fn=P.correlated_gaussian(d), num_chains=C, device=gpu, **kw)
         return k, k.init(PRNGKey(11), 4, z0, (), {})
 
     k, s = fresh()
     for _ in range(12):
-        s = k.sample(s, (), {}) if kind != "pooled" else k.sample(s)
+        s = k.sample(s, (), {}) if not pooled else k.sample(s)
     k2, s2 = fresh()
     for _ in range(7):
-        s2 = k2.sample(s2, (), {}) if kind != "pooled" else k2.sample(s2)
-    path = str(tmp_path / "ckpt.npz")
-    save_state(path, s2)
+        s2 = k2.sample(s2, (), {}) if not pooled else k2.sample(s2)
+    path = str(tmp_path / "ckpt")  # ".npz" is appended
+    marker = torch.arange(C, dtype=torch.int32, device=gpu)  # an extra array rides along
+    assert save_state(path, s2, kernel=k2, marker=marker).endswith(".npz")
     k3, _ = fresh()
-    s3 = load_state(path, gpu)
+    if kind == "pooled_overlap":
+        with pytest.raises(ValueError):
+            load_state(path, gpu)  # pending sums need the kernel that continues the run
+    s3, extra = load_state(path, gpu, kernel=k3, with_extras=True)
+    assert list(extra) == ["marker"] and np.array_equal(extra["marker"], marker.cpu().numpy())
     for _ in range(5):
-        s3 = k3.sample(s3, (), {}) if kind != "pooled" else k3.sample(s3)
+        s3 = k3.sample(s3, (), {}) if not pooled else k3.sample(s3)
     torch.cuda.synchronize()
     for a, b in zip(torch.utils._pytree.tree_leaves(s), torch.utils._pytree.tree_leaves(s3)):
         assert a.dtype == b.dtype and torch.equal(a, b)

@@ -228,6 +228,17 @@ def test_pooled_two_ranks(d, C, steps, K, overlap, world, gpu, tmp_path):
     assert zd.sum() <= max(2, C // 1000), zd.sum()
 
 
+@pytest.mark.parametrize("steps,K", [(6, 1), (48, 16)])
+def test_config5_eight_ranks_full_shape(steps, K, gpu, tmp_path):
+    """BASELINE configs[4] at its own shape: 8 ranks x 65,536 chains = 524,288,
+    d = 64, pooled every step and every 16 steps.  The ranks share the box's
+    one GPU and exchange over gloo (the RCCL path needs one GPU per rank);
+    the result equals one process holding all 524,288 chains up to the
+    association order of the all-reduced sums: L within rtol 1e-4, and at
+    most C / 1000 chains whose accept decision flips."""
+    test_pooled_two_ranks(64, 524288, steps, K, False, 8, gpu, tmp_path)
+
+
 @pytest.mark.parametrize("d,C", [(128, 700), (256, 300)])
 def test_pooled_noise_ahead_invalidation(d, C, gpu, orc):
     """Above d = 64 the update launch draws the next step's noise ahead of

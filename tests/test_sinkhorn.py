@@ -39,3 +39,23 @@ def test_default_epsilon_and_unbiased():
     a = S.sinkhorn(x, y)["cost"]
     b = S.sinkhorn(y, x)["cost"]
     assert a == pytest.approx(b, rel=1e-3)
+
+
+def test_cost_fn_objects():
+    """ott cost objects map by class name (the reference passes
+    costs.Euclidean(), evaluation.py:69); anything else is refused."""
+    from utils_amd.evaluation import _cost_mode
+
+    class Euclidean:
+        pass
+
+    class SqEuclidean:
+        pass
+
+    class Cosine:
+        pass
+
+    assert _cost_mode(Euclidean()) == "euclidean" and _cost_mode("euclidean") == "euclidean"
+    assert _cost_mode(SqEuclidean()) == "sqeuclidean" and _cost_mode("SqEuclidean") == "sqeuclidean"
+    with pytest.raises(ValueError):
+        _cost_mode(Cosine())
