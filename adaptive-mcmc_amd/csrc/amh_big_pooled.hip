@@ -36,215 +36,370 @@ __device__ __forceinline__ int64_t pk(int d, int r, int k) { return col_off(d, k
 
 // -------------------------------------------------- fused stats, d = 64 --
 // BASELINE configs[4]'s per-GPU work (d = 64, 65,536 chains): proposal,
-// potential, accept and sums in one launch, one 64-chain chunk per 256-thread block (the chunk
-// size of the d = 64 bit spec; 1,024 blocks at the config, two resident per
-// CU), with the shared factor L and the precision P staged in LDS instead of
-// read from L2 per MFMA; the blocks are persistent (two per CU) and walk the
-// chunks, so P and L are staged once per block.  Steps: z and xi -> LDS; proposal on MFMA (wave w:
-// row tile w >> 1, chain half w & 1); xprop = z + fmaf(e^lam, L xi, eps xi);
-// U(xprop) on MFMA with D = xprop - m formed as the B operand is read;
-// accept; delta = z' - mu in place of z; S_d, S_a sequential and S_dd on MFMA
-// (waves 0..2: tile pairs (0,0), (1,0), (1,1)).  Every float operation and
-// its order are those of pooled_fused_big_kernel at d = 64 (oracle:
-// orc_pooled_stats_big).
-constexpr int kF = 64;      // d
-constexpr int kFLd = 65;    // LDS row stride
-constexpr int kFChunk = 64; // chains per chunk at d = 64 (bit spec)
-constexpr size_t fused64_lds_bytes() { return ((size_t)4 * kF * kFLd + 2 * 64 + 4 * 64) * sizeof(float); }
+// potential, accept and the pooled sums of 64-chain sub-chunks, two
+// persistent 256-thread blocks per CU.  A block walks the chunks of the sums
+// (128 chains, the bit spec of every d >= 64) blockIdx.x, + gridDim.x, ..,
+// each as two sub-chunks whose fp32 sums accumulate in chain order.
+//
+// Phases per sub-chunk (wave w; lane = (i, h), i = lane & 31, h = lane >> 5):
+//   (1) noise: chains w, w + 4, ..; lane = coordinate k (arwmh.py:162-165, 174)
+//   (2) proposal on MFMA (row tile T = w >> 1, chain half w & 1):
+//       xprop = z + fmaf(e^lam, L xi, eps xi) (arwmh.py:166-167)
+//   (3) U(xprop) on MFMA, D = xprop - m formed as the B operand is read
+//   (4) accept (wave 0, lane = chain; arwmh.py:173-178)
+//   (5) z' out, delta = z' - mu
+//   (6) S_dd on MFMA (waves 0..2: tile pairs (0,0), (1,0), (1,1)), S_d and S_a
+//       sequential in chain order (wave 3); after a chunk's last sub-chunk its
+//       float32 partial row in the tile layout ([S_d | S_dd tiles in register
+//       order | 2 pad | S_a | N], 256-B stores; pooled_group4_kernel widens it
+//       exactly).
+// Operands: the A tile of L (proposal) lives in registers for the whole
+// launch (one VGPR per MFMA); P (the potential's A operand) and the B operands
+// are read from LDS arrays whose k index is stored in the MFMA's pair order, fperm(k) =
+// 32 (k & 1) + (k >> 1), so lane half h finds the k = h, h + 2, h + 4, h + 6
+// of four consecutive MFMAs in one ds_read_b128.  The next sub-chunk's z and
+// keys are loaded into registers during the current one; the barriers are
+// LDS-only (a __syncthreads() would drain those loads).
+// Oracle: orc_pooled_stats_big (float operations and their order).
+constexpr int kF = 64;       // d
+constexpr int kFS = 68;      // LDS row stride (floats): rows 16-B aligned
+constexpr int kFSub = 64;    // chains per sub-chunk
+constexpr int kFChunk = 128; // chains per chunk of the sums (bit spec, all d >= 64)
+__host__ __device__ constexpr int fperm(int k) { return (k & 1) * 32 + (k >> 1); }
+namespace f64 {  // LDS layout (floats)
+constexpr int kT = kF * kFS;
+constexpr int Z_ = 0 /* [chain][k] z */, XI = kT /* [chain][fperm k] xi, then [k][fperm chain] delta */,
+              XP = 2 * kT /* [chain][fperm k] xprop */, U_ = 3 * kT, TS = U_ + 64 /* [2][64] */, FL = TS + 128,
+              AL = FL + 64, MP = AL + 64 /* m[fperm k] */, MN = MP + 64 /* m[k] */,
+              PP = MN + 64 /* [r][fperm k] precision rows */, END = PP + kT;
+}  // namespace f64
+constexpr size_t fused64_lds_bytes() { return (size_t)f64::END * sizeof(float); }
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Diagnostic build only (make stamps, tools/f64_stamps.py): thread 0 of block
+// 0 accumulates s_memtime ticks per phase of the d = 64 fused kernel (even
+// slots: the phase's own work, odd slots: the barrier after it).
+#ifdef AMH_STAMPS
+__device__ unsigned long long g_f64_stamps[16];
+#define FS_INIT                                   \
+  unsigned long long fs_acc[16] = {0};            \
+  unsigned long long fs_prev = __builtin_amdgcn_s_memtime();
+#define FS(k)                                                 \
+  {                                                           \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime(); \
+    fs_acc[k] += t_ - fs_prev;                                \
+    fs_prev = t_;                                             \
+  }
+#define FS_FLUSH \
+  if (threadIdx.x == 0 && blockIdx.x == 0) for (int k_ = 0; k_ < 16; ++k_) g_f64_stamps[k_] = fs_acc[k_];
+hipError_t diag_f64_stamps_copy(void* host) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_f64_stamps), sizeof(unsigned long long) * 16, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define FS_INIT
+#define FS(k)
+#define FS_FLUSH
+#endif
+__device__ __forceinline__ f32x4 ld4(const float* a) { return *(const f32x4*)a; }
 
 __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParams p, int64_t n_chunks) {
-  extern __shared__ float lds[];
+  extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int d = kF;
-  constexpr int64_t P = d * (d + 1) / 2;
-  constexpr int64_t V = d + P + 2;
-  float* Pm = lds;                       // [r][k] precision rows
-  float* Lm = Pm + d * kFLd;             // [r][k] shared factor rows (0 above the diagonal)
-  float* Zb = Lm + d * kFLd;             // [k][chain] z, then delta
-  float* Xb = Zb + d * kFLd;             // [k][chain] xi, then xprop
-  float* tsum = Xb + d * kFLd;           // [2][64]
-  float* uu = tsum + 2 * 64;             // [64] uniform of the accept test
-  int* flag = (int*)(uu + 64);           // [64]
-  float* alph = (float*)(flag + 64);     // [64]
-  float* msh = alph + 64;                // [64] target mean m
+  constexpr int kSub = kFChunk / kFSub;  // sub-chunks per chunk
+  const int64_t Vt = d + 3 * 1024 + 4;   // pooled_big_tile_V(64)
+  float* Zs = lds + f64::Z_;
+  float* Xi = lds + f64::XI;
+  float* Xp = lds + f64::XP;
+  float* uu = lds + f64::U_;
+  float* tsum = lds + f64::TS;
+  int* flag = (int*)(lds + f64::FL);
+  float* alph = lds + f64::AL;
+  const float* mp = lds + f64::MP;
+  const float* mn = lds + f64::MN;
   const int tid = threadIdx.x;
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
   const int h = lane >> 5, i = lane & 31;
+  const int T = w >> 1, hf = w & 1;
+  FS_INIT
   const float c0p = p.model.data[d + d * d];
   const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
   const float el = amh_expf(p.lam[0]);
   const float mu_l = p.mu[lane];  // lane = coordinate k in the chain-major phases
-  const int T = w >> 1, hf = w & 1;  // proposal / potential: row tile, chain half
-  // P and L staged once per (persistent) block: 16 loads per thread in flight
+  // A operands in registers: lane (i, h) of MFMA m holds row 32 T + i, column 2 m + h
+  float aL[32];
   {
-    float pv[16], lv[16];
-    static_for<16>([&](auto N) {
-      const int idx = tid + 256 * N;
-      const int r = idx / d, k = idx - r * d;
-      pv[N] = p.model.data[d + idx];
-      lv[N] = (k <= r) ? p.L[pk(d, r, k)] : 0.0f;
+    // unconditional loads in one batch (above the diagonal: the row's
+    // diagonal entry, replaced by 0 once loaded); P rows to LDS in fperm order
+    const int r = 32 * T + i;
+    float pv[16];
+    static_for<32>([&](auto M) {
+      const int k = 2 * M + h;
+      aL[M] = p.L[pk(d, r, k <= r ? k : r)];
+    });
+    static_for<16>([&](auto N) { pv[N] = p.model.data[d + ((tid >> 6) + 4 * (int)N) * d + (tid & 63)]; });
+    static_for<32>([&](auto M) {
+      if (2 * M + h > r) aL[M] = 0.0f;
     });
     static_for<16>([&](auto N) {
-      const int idx = tid + 256 * N;
-      const int r = idx / d, k = idx - r * d;
-      Pm[r * kFLd + k] = pv[N];
-      Lm[r * kFLd + k] = lv[N];
+      const int row = (tid >> 6) + 4 * N, k = tid & 63;
+      lds[f64::PP + row * kFS + fperm(k)] = pv[N];
     });
-    if (tid < d) msh[tid] = p.model.data[tid];
+    if (tid < d) {
+      lds[f64::MP + fperm(tid)] = p.model.data[tid];
+      lds[f64::MN + tid] = p.model.data[tid];
+    }
   }
-  for (int64_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
-  const int64_t c0 = chunk * kFChunk;
-  const int64_t left = p.C - c0;
-  const int nv = left < kFChunk ? (int)left : kFChunk;
-  // (1) z and the noise xi (arwmh.py:162-165), k-major; wave w takes the
-  // chains w, w + 4, ..; lane = coordinate k.  All loads are issued first.
-  float pe_c = 0.0f;
-  {
-    float zv[16];
-    uint32_t k0v[16], k1v[16];
+  // the block's sub-chunks, flat: t -> chunk blockIdx.x + gridDim.x (t / kSub),
+  // sub-chunk t % kSub; only the grid's last chunk can be ragged, so the valid
+  // ones are a prefix
+  const int64_t G = gridDim.x;
+  int64_t nmine = 0;
+  if ((int64_t)blockIdx.x < n_chunks) {
+    const int64_t nchk = (n_chunks - 1 - (int64_t)blockIdx.x) / G + 1;
+    const int64_t last_c0 = ((int64_t)blockIdx.x + G * (nchk - 1)) * kFChunk;
+    const int64_t last_subs = (p.C - last_c0 + kFSub - 1) / kFSub;
+    nmine = kSub * (nchk - 1) + (last_subs < kSub ? last_subs : kSub);
+  }
+  auto sub_c0 = [&](int64_t t) { return ((int64_t)blockIdx.x + G * (t / kSub)) * kFChunk + kFSub * (t % kSub); };
+  // z and keys of a sub-chunk's chains w + 4 N (lane = coordinate; the key's
+  // two words alternate over the lanes and come back with v_readlane), pe of
+  // its chains (wave 0, lane = chain)
+  // (keys: lane l < 32 holds word l >> 4 of chain w + 4 (l & 15); one VGPR;
+  // lanes 0..15 hold the noise record of chain w + 4 lane when noise drawn
+  // ahead exists: (i, key0, key1, u bits))
+  float zr[16];
+  uint32_t kr = 0u;
+  uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+  float pev = 0.0f;
+  const bool ahead = p.xi != nullptr;
+  auto load_sub = [&](int64_t t) {
+    const int64_t c0 = sub_c0(t);
     static_for<16>([&](auto N) {
       int64_t ch = c0 + w + 4 * N;
       if (ch >= p.C) ch = p.C - 1;
-      zv[N] = p.z[ch * d + lane];
-      k0v[N] = p.keys[2 * ch];
-      k1v[N] = p.keys[2 * ch + 1];
+      zr[N] = p.z[ch * d + lane];
     });
-    pe_c = (tid < nv) ? p.pe[c0 + tid] : 0.0f;
-    __syncthreads();  // the previous chunk's readers of Zb / Xb / uu are done
-    static_for<16>([&](auto N) {
-      const int cc = w + 4 * N;
-      Zb[lane * kFLd + cc] = zv[N];
-#ifndef AMH_F64_NORNG
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)it, 0u, AMH_TAG_STEP, k0v[N], k1v[N]);
-      Xb[lane * kFLd + cc] = amh_normal_from_bits(o.v[0]);
-      if (lane == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
-#else
-      Xb[lane * kFLd + cc] = (float)((k0v[N] + lane) & 15) * 0.1f - 0.75f;
-      if (lane == 0) uu[cc] = 0.5f;
-#endif
-    });
+    int64_t kc = c0 + w + 4 * (lane & 15);
+    if (kc >= p.C) kc = p.C - 1;
+    kr = p.keys[2 * kc + ((lane >> 4) & 1)];
+    if (ahead) rec = (kc < p.xi_cap) ? p.xrec[kc] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
+  };
+  auto load_pe = [&](int64_t t) {
+    const int64_t c0 = sub_c0(t);
+    pev = (w == 0 && c0 + lane < p.C) ? p.pe[c0 + lane] : 0.0f;
+  };
+  auto store_z = [&]() { static_for<16>([&](auto N) { Zs[(w + 4 * N) * kFS + lane] = zr[N]; }); };
+  f32x16 sacc = f32x16{};  // S_dd of the chunk so far (waves 0..2)
+  float sd = 0.0f, sa = 0.0f;  // S_d (wave 3, lane = coordinate), S_a (wave 3 lane 0)
+  int cnt = 0;
+  if (nmine > 0) {
+    load_sub(0);
+    load_pe(0);
+    store_z();
   }
-  __syncthreads();
-  // (2) proposal: acc = L xi over k < 32 (T + 1) (arwmh.py:166-167)
-  {
-    f32x16 acc = f32x16{};
-    const int kend = 32 * (T + 1);
-    const int arow = (32 * T + i) * kFLd + h;
-#ifndef AMH_F64_NOPROP
-    for (int kk = 0; kk < kend; kk += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Lm[arow + kk], Xb[(kk + h) * kFLd + 32 * hf + i], acc, 0, 0, 0);
-#endif
-    float v[16];
-    static_for<16>([&](auto R) {
-      const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
-      v[R] = fmaf(el, acc[(int)R], p.eps * Xb[rr * kFLd + 32 * hf + i]);
-    });
-    __syncthreads();
-    static_for<16>([&](auto R) {
-      const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
-      const int o = rr * kFLd + 32 * hf + i;
-      Xb[o] = Zb[o] + v[R];  // xprop = z + (e^lam L xi + eps xi)
-    });
-  }
-  __syncthreads();
-  // (3) U(xprop) on MFMA: Y = P D with D = xprop - m, q_r = D_r y_r
-  {
-    f32x16 acc = f32x16{};
-    const int arow = (32 * T + i) * kFLd + h;
-#ifndef AMH_F64_NOPOT
-    for (int kk = 0; kk < d; kk += 2)
-      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(Pm[arow + kk], Xb[(kk + h) * kFLd + 32 * hf + i] - msh[kk + h], acc,
-                                                 0, 0, 0);
-#endif
-    float ps = 0.0f;
-    static_for<16>([&](auto R) {
-      const int row = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
-      ps = ps + (Xb[row * kFLd + 32 * hf + i] - msh[row]) * acc[(int)R];
-    });
-    const float other = __shfl_xor(ps, 32, 64);
-    const float tI = (h == 0) ? ps + other : other + ps;
-    if (h == 0) tsum[T * 64 + 32 * hf + i] = tI;
-  }
-  __syncthreads();
-  // (4) accept / reject (arwmh.py:173-178)
-  if (tid < 64) {
-    int acc_f = 0;
-    float a = 0.0f;
-    if (tid < nv) {
-      float S = 0.0f;
-      S = S + tsum[tid];
-      S = S + tsum[64 + tid];
-      float pp = (0.5f * S) + c0p;
-      if (amh_isnan(pp)) pp = INFINITY;
-      const float ex = amh_expf(pe_c - pp);
-      a = (ex > 1.0f) ? 1.0f : ex;
-      acc_f = uu[tid] < a;
-      p.pe_out[c0 + tid] = acc_f ? pp : pe_c;
+  lds_barrier();
+  FS(14)
+  for (int64_t t = 0; t < nmine; ++t) {
+    const int64_t c0 = sub_c0(t);
+    const int64_t left = p.C - c0;
+    const int nv = left < kFSub ? (int)left : kFSub;
+    // ---- (1) noise of chains w + 4 N: drawn ahead by the previous update
+    // launch when the chain's record is this draw's (i, key), else here
+    uint64_t usem = 0;
+    if (ahead) {
+      // lane N < 16: key word 0 of chain N is its own kr, word 1 lane N + 16's
+      const uint32_t kw1 = (uint32_t)__shfl_down((int)kr, 16, 64);
+      const bool ok = (lane < 16) && rec.x == (uint32_t)it && rec.y == kr && rec.z == kw1;
+      usem = __ballot(ok);
     }
-    flag[tid] = acc_f;
-    alph[tid] = a;
-  }
-  __syncthreads();
-  // (5) z' out, delta = z' - mu in place of z (k-major)
-  static_for<16>([&](auto N) {
-    const int cc = w + 4 * N;
-    float dv = 0.0f;
-    if (cc < nv) {
-      const float zn = flag[cc] ? Xb[lane * kFLd + cc] : Zb[lane * kFLd + cc];
-      p.z_out[(c0 + cc) * d + lane] = zn;
-      dv = zn - mu_l;
-    }
-    Zb[lane * kFLd + cc] = dv;
-  });
-  __syncthreads();
-  // (6) the chunk's sums: S_d, S_a sequential over chains, S_dd on MFMA
-  double* out = p.partials + chunk * V;
-  // sequential adds in chain order, LDS reads batched 16 at a time (slots
-  // past nv hold +0: adding +0 to a sum that started at +0 changes no bit)
-  if (tid < d) {
-    float sd = 0.0f;
-    static_for<4>([&](auto B) {
-      float x[16];
-      static_for<16>([&](auto Q) { x[Q] = Zb[tid * kFLd + 16 * B + Q]; });
-      static_for<16>([&](auto Q) { sd = sd + x[Q]; });
-    });
-    out[tid] = (double)sd;
-  }
-  if (tid == 64) {
-    float sa = 0.0f;
-    static_for<4>([&](auto B) {
-      float x[16];
-      static_for<16>([&](auto Q) { x[Q] = alph[16 * B + Q]; });
-      static_for<16>([&](auto Q) { sa = sa + x[Q]; });
-    });
-    out[d + P] = (double)sa;
-    out[d + P + 1] = (double)nv;
-  }
-#ifndef AMH_F64_NOSDD
-  if (w < 3) {
-#else
-  if (w < 0) {
-#endif
-    const int pI = (w == 0) ? 0 : 1, pJ = (w == 2) ? 1 : 0;
-    const int ra = (32 * pI + i) * kFLd, rb = (32 * pJ + i) * kFLd;
-    f32x16 sacc = f32x16{};
-    int kk = 0;
-    for (; kk + 16 <= nv; kk += 16) {
-      float a[8], b[8];
-      static_for<8>([&](auto Q) {
-        a[Q] = Zb[ra + kk + 2 * Q + h];
-        b[Q] = Zb[rb + kk + 2 * Q + h];
+    if (usem == 0xFFFFull) {  // every chain of the wave: rows of the buffer (one latency)
+      float xr[16];
+      static_for<16>([&](auto N) {
+        int64_t ch = c0 + w + 4 * N;
+        if (ch >= p.C) ch = p.C - 1;
+        xr[N] = p.xi[ch * d + lane];
       });
-      static_for<8>([&](auto Q) { sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[Q], b[Q], sacc, 0, 0, 0); });
+      static_for<16>([&](auto N) {
+        const int cc = w + 4 * N;
+        Xi[cc * kFS + fperm(lane)] = xr[N];
+        const uint32_t ub = (uint32_t)__builtin_amdgcn_readlane((int)rec.w, N);
+        if (lane == 0) uu[cc] = amh_unif01_from_bits(ub);
+      });
+    } else {
+      static_for<16>([&](auto N) {
+        const int cc = w + 4 * N;
+        if ((usem >> N) & 1) {
+          int64_t ch = c0 + cc;
+          Xi[cc * kFS + fperm(lane)] = p.xi[ch * d + lane];
+          const uint32_t ub = (uint32_t)__builtin_amdgcn_readlane((int)rec.w, N);
+          if (lane == 0) uu[cc] = amh_unif01_from_bits(ub);
+        } else {
+          const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)kr, N);
+          const uint32_t k1 = (uint32_t)__builtin_amdgcn_readlane((int)kr, 16 + N);
+          const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+          Xi[cc * kFS + fperm(lane)] = amh_normal_from_bits(o.v[0]);
+          if (lane == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
+        }
+        if constexpr (N % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // four chains interleaved at most
+      });
     }
-    for (; kk < nv; kk += 2) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(Zb[ra + kk + h], Zb[rb + kk + h], sacc, 0, 0, 0);
-    static_for<16>([&](auto R) {
-      const int row = 32 * pI + (R & 3) + 8 * (R >> 2) + 4 * h;
-      const int col = 32 * pJ + i;
-      if (row >= col) out[d + pk(d, row, col)] = (double)sacc[(int)R];
-    });
+    const bool more = t + 1 < nmine;
+    if (more) load_sub(t + 1);  // in flight through phases (2) .. (6)
+    FS(0)
+    lds_barrier();
+    FS(1)
+    // ---- (2) proposal: acc = L xi over k < 32 (T + 1)
+    {
+      f32x16 acc = f32x16{};
+      const float* bp = Xi + (32 * hf + i) * kFS + 32 * h;
+      static_for<8>([&](auto G4) {
+        if (G4 < 4 * (T + 1)) {
+          const f32x4 bv = ld4(bp + 4 * G4);
+          static_for<4>([&](auto Q) { acc = __builtin_amdgcn_mfma_f32_32x32x2f32(aL[4 * G4 + Q], bv[(int)Q], acc, 0, 0, 0); });
+        }
+      });
+      const int ch = 32 * hf + i;
+      static_for<16>([&](auto R) {
+        const int rr = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+        const float v = fmaf(el, acc[(int)R], p.eps * Xi[ch * kFS + fperm(rr)]);
+        Xp[ch * kFS + fperm(rr)] = Zs[ch * kFS + rr] + v;  // xprop = z + (e^lam L xi + eps xi)
+      });
+    }
+    FS(2)
+    lds_barrier();
+    FS(3)
+    // ---- (3) U(xprop) on MFMA: Y = P D with D = xprop - m, q_r = D_r y_r
+    {
+      f32x16 acc = f32x16{};
+      const int ch = 32 * hf + i;
+      const float* bp = Xp + ch * kFS + 32 * h;
+      const float* ap = lds + f64::PP + (32 * T + i) * kFS + 32 * h;
+      static_for<8>([&](auto G4) {
+        const f32x4 av = ld4(ap + 4 * G4);
+        const f32x4 xv = ld4(bp + 4 * G4);
+        const f32x4 mv = ld4(mp + 32 * h + 4 * G4);
+        static_for<4>([&](auto Q) {
+          acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[(int)Q], xv[(int)Q] - mv[(int)Q], acc, 0, 0, 0);
+        });
+      });
+      float ps = 0.0f;
+      static_for<16>([&](auto R) {
+        const int row = 32 * T + (R & 3) + 8 * (R >> 2) + 4 * h;
+        ps = ps + (Xp[ch * kFS + fperm(row)] - mn[row]) * acc[(int)R];
+      });
+      const float other = __shfl_xor(ps, 32, 64);
+      const float tI = (h == 0) ? ps + other : other + ps;
+      if (h == 0) tsum[T * 64 + ch] = tI;
+    }
+    FS(4)
+    lds_barrier();
+    FS(5)
+    // ---- (4) accept / reject
+    if (w == 0) {
+      int acc_f = 0;
+      float a = 0.0f;
+      if (lane < nv) {
+        float S = 0.0f;
+        S = S + tsum[lane];
+        S = S + tsum[64 + lane];
+        float pp = (0.5f * S) + c0p;
+        if (amh_isnan(pp)) pp = INFINITY;
+        const float ex = amh_expf(pev - pp);
+        a = (ex > 1.0f) ? 1.0f : ex;
+        acc_f = uu[lane] < a;
+        p.pe_out[c0 + lane] = acc_f ? pp : pev;
+      }
+      flag[lane] = acc_f;
+      alph[lane] = a;
+      if (more) load_pe(t + 1);
+    }
+    FS(6)
+    lds_barrier();
+    FS(7)
+    // ---- (5) z' out, delta = z' - mu as [k][fperm chain] over the xi array
+    //      (every LDS read first, then the stores)
+    {
+      float zn[16];
+      static_for<16>([&](auto N) {
+        const int cc = w + 4 * N;
+        const float xp = Xp[cc * kFS + fperm(lane)], zo = Zs[cc * kFS + lane];
+        zn[N] = flag[cc] ? xp : zo;
+      });
+      static_for<16>([&](auto N) {
+        const int cc = w + 4 * N;
+        float dv = 0.0f;
+        if (cc < nv) {
+          p.z_out[(c0 + cc) * d + lane] = zn[N];
+          dv = zn[N] - mu_l;
+        }
+        Xi[lane * kFS + fperm(cc)] = dv;
+      });
+    }
+    FS(8)
+    lds_barrier();
+    FS(9)
+    // ---- (6) the chunk's sums, accumulated over its sub-chunks in chain order
+    {
+      const bool last = (t % kSub == kSub - 1) || !more;  // the chunk's last sub-chunk
+      float* out = (float*)p.partials + (c0 / kFChunk) * Vt;
+      if (w < 3) {
+        const int pI = (w == 0) ? 0 : 1, pJ = (w == 2) ? 1 : 0;
+        const float* ap = Xi + (32 * pI + i) * kFS + 32 * h;
+        const float* bp = Xi + (32 * pJ + i) * kFS + 32 * h;
+        if (nv == kFSub) {
+          static_for<8>([&](auto G4) {
+            const f32x4 av = ld4(ap + 4 * G4), bv = ld4(bp + 4 * G4);
+            static_for<4>([&](auto Q) { sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(av[(int)Q], bv[(int)Q], sacc, 0, 0, 0); });
+          });
+        } else {
+          // ragged tail: chain pairs (2m, 2m + 1) for 2m < nv (a chain past nv
+          // in the last pair holds delta = +0)
+          for (int m = 0; 2 * m < nv; ++m) sacc = __builtin_amdgcn_mfma_f32_32x32x2f32(ap[m], bp[m], sacc, 0, 0, 0);
+        }
+        if (last) {
+          float* o = out + d + (int64_t)w * 1024 + lane;  // pair index I (I + 1) / 2 + J = w
+          static_for<16>([&](auto R) { o[64 * R] = sacc[(int)R]; });
+          sacc = f32x16{};
+        }
+      } else {
+        // sequential adds in chain order (slots past nv hold +0: adding +0 to a
+        // sum that started at +0 changes no bit); even chains at fperm 0..31,
+        // odd ones at 32..63
+        const float* rp = Xi + lane * kFS;
+        static_for<8>([&](auto G4) {
+          const f32x4 ev = ld4(rp + 4 * G4), ov = ld4(rp + 32 + 4 * G4);
+          static_for<4>([&](auto Q) {
+            sd = sd + ev[(int)Q];
+            sd = sd + ov[(int)Q];
+          });
+        });
+        if (lane == 0) {
+          static_for<16>([&](auto G4) {
+            const f32x4 av = ld4(alph + 4 * G4);
+            static_for<4>([&](auto Q) { sa = sa + av[(int)Q]; });
+          });
+        }
+        cnt += nv;
+        if (last) {
+          out[lane] = sd;
+          if (lane == 0) {
+            out[Vt - 2] = sa;
+            out[Vt - 1] = (float)cnt;
+          }
+          sd = 0.0f;
+          sa = 0.0f;
+          cnt = 0;
+        }
+      }
+    }
+    if (more) store_z();  // every wave is past its phase-(5) reads of z
+    FS(10)
+    lds_barrier();
+    FS(11)
   }
-  }  // chunks
+  FS_FLUSH
 }
 
 // --------------------------------------------------- fused stats, d > 64 --
@@ -795,19 +950,39 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
   const float lamn = lam + gamma * (abar - p.target);
   // (0) A = float((1-g) Sigma + g S_dd / N), formed in the 4-row-aligned
   // layout by pooled_big_prep_kernel (all CUs): one coalesced 16-B copy.
-  // d = 64 (2,080 entries) forms it here, a wave per column, with the same
-  // double arithmetic (one launch instead of three, see (4))
+  // d = 64 (2,080 entries) forms it here, wave w for columns w + 16 q, lane
+  // = row offset, with the same double arithmetic (one launch instead of
+  // three, see (4)).  Every global operand of the d = 64 update -- the old
+  // covariance and factor for the write-out, S_d and mu for the mean -- is
+  // loaded here in one batch and kept in registers (one memory latency
+  // instead of one per phase and column).
+  constexpr int kQ = NT == 2 ? d / kUpdWaves : 1;
+  double sig[kQ], cvo[kQ];
+  float lvo[kQ];
+  float loc_in = 0.0f;
+  double sd_in = 0.0;
   if constexpr (NT == 2) {
+    static_assert(d % kUpdWaves == 0, "d = 64: whole columns per wave");
     const double g = (double)gamma;
-    for (int k = w; k < d; k += kUpdWaves) {
-      const int64_t co = col_off(d, k);
-      const int ab = a4_base(d, k);
-      if (lane < d - k) {
-        const double a = (1.0 - g) * p.in.cov[co + lane];
-        const double b = g * (sums[d + co + lane] / N);
-        A[ab + k + lane] = (float)(a + b);
-      }
+    double sv[kQ];
+    static_for<kQ>([&](auto Q) {
+      const int k = w + kUpdWaves * Q;
+      const int64_t o = col_off(d, k) + (lane < d - k ? lane : 0);
+      cvo[Q] = p.in.cov[o];
+      sv[Q] = sums[d + o];
+      lvo[Q] = p.in.scale[o];
+    });
+    if (tid < d) {
+      loc_in = p.in.loc[tid];
+      sd_in = sums[tid];
     }
+    static_for<kQ>([&](auto Q) {
+      const int k = w + kUpdWaves * Q;
+      const double a = (1.0 - g) * cvo[Q];
+      const double b = g * (sv[Q] / N);
+      sig[Q] = a + b;
+      if (lane < d - k) A[a4_base(d, k) + k + lane] = (float)sig[Q];
+    });
   } else {
     const int nA = d * (d + 4) / 2;
     const f32x4* src = (const f32x4*)p.scratch;
@@ -940,31 +1115,24 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     // ops and sum order (a column's rows fit one wave, so of its 256-lane
     // big_sum only the first 64-lane butterfly is non-zero)
     __shared__ float colsum[64];
-    const double g = (double)gamma;
     const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
-    for (int k = w; k < d; k += kUpdWaves) {
+    static_for<kQ>([&](auto Q) {
+      const int k = w + kUpdWaves * Q;
       const int64_t co = col_off(d, k);
       const int ab = a4_base(d, k);
       float sq = 0.0f;
       if (lane < d - k) {
         const int64_t o = co + lane;
-        const float lo = p.in.scale[o];
+        const float lo = lvo[Q];
         const float ln = ok ? A[ab + k + lane] : lo;
         const float tt = (ln * e1) - (lo * e0);
         sq = tt * tt;
-        if (ok) {
-          const double a = (1.0 - g) * p.in.cov[o];
-          const double b = g * (sums[d + o] / N);
-          p.out.cov[o] = a + b;
-          p.out.scale[o] = ln;
-        } else {
-          p.out.cov[o] = p.in.cov[o];
-          p.out.scale[o] = lo;
-        }
+        p.out.cov[o] = ok ? sig[Q] : cvo[Q];
+        p.out.scale[o] = ln;
       }
       const float s0 = Grp<64>::sum(sq);
       if (lane == 0) colsum[k] = (s0 + 0.0f) + (0.0f + 0.0f);
-    }
+    });
     __syncthreads();
     if (w == 0) {
       const float S = Grp<64>::sum(colsum[lane]);
@@ -995,7 +1163,190 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     }
   }
   }
-  if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
+  if constexpr (NT == 2) {
+    if (tid < d) p.out.loc[tid] = loc_in + gamma * (float)(sd_in / N);
+  } else {
+    if (tid < d) p.out.loc[tid] = p.in.loc[tid] + gamma * (float)(sums[tid] / N);
+  }
+  US(4)
+  US_FLUSH
+}
+
+// d = 64 (BASELINE configs[4]): the whole shared-state update in one
+// 256-thread workgroup.  Every global operand (Sigma, S_dd, the old factor,
+// S_d, mu) is loaded in one batch by the four waves (wave w: columns w + 4 q,
+// lane = row offset), Sigma' = (1-g) Sigma + g S_dd / N is formed in double
+// and rounded into LDS row by row, then wave 0 factors it with lane r holding
+// row r in 64 registers: column k's pivot comes from lane k (v_readlane),
+// L_kk = sqrtf, the column is divided, column k's update of column k + 1
+// follows through v_readlane (the next pivot is then ready), and its update
+// of the columns beyond arrives through a 64-float LDS broadcast applied
+// after the next column's pivot and division (software-pipelined; per
+// element the oracle's fmaf chain in column order, so the bits are those of
+// the panel kernel it replaces and of orc_pooled_update_big).  The write-out
+// and as_change (column sums by the 64-lane butterfly, then the columns)
+// follow on all four waves.
+__global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams p) {
+  constexpr int d = 64, P = d * (d + 1) / 2, kQ = d / 4;
+  constexpr int S = d + 1;  // LDS row stride of the factor
+  __shared__ float A[d * S];
+  __shared__ __attribute__((aligned(16))) float cb[2][64];
+  __shared__ float colsum[64];
+  __shared__ int okv;
+  if (blockIdx.x > 0) {
+    // extra blocks (one 8-wave block per other CU) beside the single-workgroup
+    // update: the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
+    // Philox(0, i', 0)[1] of every chain, i' = i + K, each chain's row with
+    // its record (the stats kernel uses a row only if the record is its draw)
+    const int32_t inext = p.in.i[0] + p.K;
+    const int lane = lane_id();
+    // wave wv takes the chains wv, wv + nw, ..; the keys of 32 of them arrive
+    // in one vector load (lane l: word l & 1 of the (l >> 1)-th)
+    const int64_t wv = (int64_t)(blockIdx.x - 1) * 8 + threadIdx.x / 64;
+    const int64_t nw = (int64_t)(gridDim.x - 1) * 8;
+    for (int64_t c32 = wv; c32 < p.noise_C; c32 += 32 * nw) {
+      int64_t kc = c32 + nw * (lane >> 1);
+      if (kc >= p.noise_C) kc = p.noise_C - 1;
+      const uint32_t kv = p.keys[2 * kc + (lane & 1)];
+      static_for<32>([&](auto J) {
+        const int64_t ch = c32 + nw * J;
+        if (ch < p.noise_C) {
+          const uint32_t kk0 = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J);
+          const uint32_t kk1 = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J + 1);
+          const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0, kk1);
+          p.xi[ch * d + lane] = amh_normal_from_bits(o.v[0]);
+          const uint32_t ubits = (uint32_t)__builtin_amdgcn_readlane((int)o.v[1], 0);
+          if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0, kk1, ubits);
+        }
+        if constexpr (J % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      });
+    }
+    return;
+  }
+  if (threadIdx.x >= 256) return;  // block 0: four waves, the CU to themselves
+  if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);  // the factorisation wave first on its SIMD
+  const int tid = threadIdx.x;
+  US_INIT
+  const int lane = lane_id();
+  const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
+  const double* sums = p.sums;
+  // (0) one batch of loads (issued before anything waits on the scalars)
+  double sig[kQ], cvo[kQ], sv[kQ];
+  float lvo[kQ];
+  static_for<kQ>([&](auto Q) {
+    const int k = w + 4 * Q;
+    const int64_t o = col_off(d, k) + (lane < d - k ? lane : 0);
+    cvo[Q] = p.in.cov[o];
+    sv[Q] = sums[d + o];
+    lvo[Q] = p.in.scale[o];
+  });
+  const float loc_in = p.in.loc[lane];
+  const double sd_in = sums[lane];
+  const double N = sums[d + P + 1];
+  const int32_t it = p.in.i[0];
+  const int32_t itr = it + p.K;
+  const int32_t n = pooled_block_n(it, p.W, p.K);
+  const float gamma = amh_lr_gamma(n, p.a);
+  const float macc = p.in.mean_accept_prob[0];
+  const float lam = p.in.log_step_size[0];
+  const float abar = (float)(sums[d + P] / N);
+  const float maccn = macc + (abar - macc) / (float)n;
+  const float lamn = lam + gamma * (abar - p.target);
+  // Sigma' in double, rounded into LDS rows
+  {
+    const double g = (double)gamma;
+    static_for<kQ>([&](auto Q) {
+      const int k = w + 4 * Q;
+      const double a = (1.0 - g) * cvo[Q];
+      const double b = g * (sv[Q] / N);
+      sig[Q] = a + b;
+      if (lane < d - k) A[(k + lane) * S + k] = (float)sig[Q];
+    });
+  }
+  US(0)
+  __syncthreads();
+  US(1)
+  // (1) the factorisation on wave 0 (entries above the diagonal are never
+  // read as operands of valid ones: lanes r < k compute values that are unused)
+  if (w == 0) {
+    int ln = lane;  // opaque: keeps the per-column lane tests from being hoisted
+    asm volatile("" : "+v"(ln));
+    float a[d];
+    static_for<d>([&](auto K) { a[K] = A[ln * S + K]; });
+    bool ok = true;
+    f32x4 pv[16];  // column k-1's broadcast (rows 4Q .. 4Q+3)
+    float am1 = 0.0f;
+    static_for<d>([&](auto K) {
+      constexpr int k = K;
+      const float piv = rdlane(a[k], k);
+      ok = ok && (piv > 0.0f) && amh_isfinite(piv);
+      const float ljj = sqrtf(piv);
+      const float q = a[k] / ljj;
+      __builtin_amdgcn_sched_barrier(0);
+      if constexpr (k >= 1) {  // column k-1's updates of the columns m >= k+1
+        static_for<16>([&](auto Q) {
+          static_for<4>([&](auto E) {
+            constexpr int m = 4 * Q + E;
+            if constexpr (m >= k + 1) a[m] = fmaf(-am1, pv[(int)Q][(int)E], a[m]);
+          });
+        });
+      }
+      a[k] = (ln == k) ? ljj : q;
+      if constexpr (k + 1 < d) {
+        float* cbk = cb[k & 1];
+        cbk[ln] = a[k];
+        static_for<16>([&](auto Q) {
+          if constexpr (4 * Q + 3 >= k + 2) pv[(int)Q] = *(const f32x4*)&cbk[4 * Q];
+        });
+        am1 = a[k];
+        const float l1 = rdlane(a[k], k + 1);
+        a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    static_for<d>([&](auto K) {
+      if ((int)K <= ln) A[ln * S + K] = a[K];
+    });
+    if (lane == 0) okv = ok ? 1 : 0;
+  }
+  US(2)
+  __syncthreads();
+  US(3)
+  // (2) write-out and as_change: column k's squared terms (rows k + t) by the
+  // 64-lane butterfly, then the columns (pooled_big_post_kernel's order)
+  const bool ok = okv != 0;
+  const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
+  float sq[kQ];
+  static_for<kQ>([&](auto Q) {
+    const int k = w + 4 * Q;
+    const int64_t co = col_off(d, k);
+    sq[Q] = 0.0f;
+    const float lf = A[((k + lane) < d ? k + lane : d - 1) * S + k];
+    if (lane < d - k) {
+      const int64_t o = co + lane;
+      const float lo = lvo[Q];
+      const float lnw = ok ? lf : lo;
+      const float tt = (lnw * e1) - (lo * e0);
+      sq[Q] = tt * tt;
+      p.out.cov[o] = ok ? sig[Q] : cvo[Q];
+      p.out.scale[o] = lnw;
+    }
+  });
+  static_for<kQ>([&](auto Q) {  // independent butterflies, interleaved
+    const float s0 = Grp<64>::sum(sq[Q]);
+    if (lane == 0) colsum[w + 4 * Q] = (s0 + 0.0f) + (0.0f + 0.0f);
+  });
+  __syncthreads();
+  if (w == 0) {
+    const float Ssum = Grp<64>::sum(colsum[lane]);
+    if (lane == 0) {
+      p.out.as_change[0] = sqrtf((Ssum + 0.0f) + (0.0f + 0.0f));
+      p.out.i[0] = itr;
+      p.out.mean_accept_prob[0] = maccn;
+      p.out.log_step_size[0] = lamn;
+    }
+  }
+  if (w == 0) p.out.loc[lane] = loc_in + gamma * (float)(sd_in / N);
   US(4)
   US_FLUSH
 }
@@ -1107,11 +1458,12 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const int64_t grid = nch < 2 * (int64_t)cus ? nch : 2 * (int64_t)cus;  // persistent: P, L staged once per block
+    const int64_t grid = nch < 2 * (int64_t)cus ? nch : 2 * (int64_t)cus;  // persistent, two per CU
     hipLaunchKernelGGL(pooled_fused64_kernel, dim3((unsigned)grid), dim3(256), fused64_lds_bytes(), s, p, nch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return pooled_reduce(p.partials, nch, V, sums, p.accumulate, s);
+    (void)V;
+    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d);
   }
   {
     const int nt = d / 32;
@@ -1151,6 +1503,17 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, boo
     hipLaunchKernelGGL(pooled_big_prep_kernel, dim3((unsigned)p.d), dim3(256), 0, s, p);
     e = hipGetLastError();
     if (e != hipSuccess) return e;
+  }
+  if (p.d == 64) {
+    unsigned nb = 1;  // + one noise block per other CU when the next step's noise is drawn ahead
+    if (p.noise_C > 0 && p.xi != nullptr) {
+      int dev = 0, cus = 0;
+      (void)hipGetDevice(&dev);
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      nb = (unsigned)(cus > 1 ? cus : 2);
+    }
+    hipLaunchKernelGGL(pooled_update64_kernel, dim3(nb), dim3(512), 0, s, p);
+    return hipGetLastError();
   }
   unsigned nblk = 1;  // + one noise block per other CU when the next step's noise is drawn ahead
   if (p.noise_C > 0 && p.xi != nullptr) {

@@ -547,7 +547,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
   const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains, d) : (num_chains + chunk - 1) / chunk;
-  const int64_t vrow = (big && d != 64) ? amh::pooled_big_tile_V(d) : d + (int64_t)d * (d + 1) / 2 + 2;
+  const int64_t vrow = big ? amh::pooled_big_tile_V(d) : d + (int64_t)d * (d + 1) / 2 + 2;
   const size_t need = (size_t)amh::pooled_scratch_rows(n_chunks) * (size_t)vrow * sizeof(double);
   if (need > h->partials_bytes) {
     if (h->partials) {
@@ -582,7 +582,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
     h->big_ready_C = -1;
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;
-    if (d != 64) {
+    {
       // noise drawn ahead by the update launch (records checked per chain
       // by the stats kernel, so a stale or foreign buffer is never used)
       const size_t nn = (size_t)num_chains * (16 + (size_t)d * sizeof(float));
@@ -687,7 +687,7 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipMemsetAsync");
     }
     p.scratch = h->upd_buf;
-    if (p.d != 64 && h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys) {
+    if (h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys) {
       p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows
       p.keys = (const uint32_t*)in->rng_key;
       p.xrec = (uint4*)h->noise_buf;
@@ -737,5 +737,7 @@ int amh_diag_stamps(void* host, int64_t bytes) {
 }
 // pooled large-d update kernel phase totals (8 x u64)
 int amh_diag_upd_stamps(void* host) { return amh::diag_upd_stamps_copy(host) == hipSuccess ? 0 : -1; }
+// pooled d = 64 fused stats kernel phase totals (16 x u64, block 0 thread 0)
+int amh_diag_f64_stamps(void* host) { return amh::diag_f64_stamps_copy(host) == hipSuccess ? 0 : -1; }
 #endif
 }  // extern "C"

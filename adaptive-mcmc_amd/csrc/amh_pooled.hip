@@ -300,23 +300,14 @@ __device__ __forceinline__ int fp_a4_base(int d, int j) {
   return 4 * (q * d - 2 * q * (q - 1)) + (j & 3) * (d - 4 * q) - (j & ~3);
 }
 
-__global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
-                                                           double* sums, int accumulate, int tile_d, FinalPrep fp) {
-  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (u >= V) return;
+// entry u of the sums once its total over the groups is known: the packed
+// index (tile layout above d = 64), accumulation over the steps of a pooled
+// block, and (one rank, amh_pooled_step_k) the update's Sigma' entry
+__device__ __forceinline__ void final_entry(int64_t u, double tot, int64_t V, double* sums, int accumulate,
+                                            int tile_d, const FinalPrep& fp) {
   int row = -1, col = -1;
   const int64_t v = tile_d ? tile_to_packed(u, V, tile_d, &row, &col) : u;
   if (v < 0) return;
-  double tot = 0.0;
-  int64_t g = 0;
-  for (; g + 8 <= n_groups; g += 8) {  // loads in flight, adds in group order
-    double x[8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) x[q] = gsum[(g + q) * V + u];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) tot += x[q];
-  }
-  for (; g < n_groups; ++g) tot += gsum[g * V + u];
   const double sv = accumulate ? sums[v] + tot : tot;
   sums[v] = sv;
   if (fp.scratch != nullptr && col >= 0) {
@@ -330,6 +321,31 @@ __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restr
     fp.scratch[fp_a4_base(d, col) + row] = (float)(a + b);
     if (u == d) ((int*)fp.scratch)[d * (d + 4) / 2 + 4] = it + fp.K;  // the next step's i (noise blocks)
   }
+}
+
+__global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
+                                                           double* sums, int accumulate, int tile_d, FinalPrep fp) {
+  const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (u >= V) return;
+  if (tile_d && tile_to_packed(u, V, tile_d) < 0) return;
+  double tot = 0.0;
+  int64_t g = 0;
+  for (; g + 32 <= n_groups; g += 32) {  // 32 loads in flight, adds in group order
+    double x[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) x[q] = gsum[(g + q) * V + u];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) tot += x[q];
+  }
+  for (; g + 8 <= n_groups; g += 8) {
+    double x[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) x[q] = gsum[(g + q) * V + u];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tot += x[q];
+  }
+  for (; g < n_groups; ++g) tot += gsum[g * V + u];
+  final_entry(u, tot, V, sums, accumulate, tile_d, fp);
 }
 
 int64_t pooled_scratch_rows(int64_t n_chunks) { return n_chunks + (n_chunks + kRedGroup - 1) / kRedGroup; }

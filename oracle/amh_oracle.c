@@ -1114,16 +1114,16 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
  *  proposal  z' = z + fmaf(e^lam, acc, eps xi), acc_r = fmaf chain over
  *            k < 32 (floor(r / 32) + 1) of L_rk xi_k (L_rk = 0 above the
  *            diagonal; MFMA on 32-row tiles), U(z') in the MFMA order.
- *  sums      chunks of 256 (d = 64: 64) consecutive chains: float32 S_dd (fmaf chain over
+ *  sums      chunks of 128 consecutive chains: float32 S_dd (fmaf chain over
  *            the chunk's chains in order, MFMA), S_d and S_a (sequential
  *            adds), written in double; chunks reduced as in the d <= 64 mode.
  *  update    Sigma' in double as the d <= 64 mode; its Cholesky factor in
  *            float32 (element (r, k) updated in column order j < k, then
  *            divided by L_kk = sqrtf(A_kk)); as_change: squared terms of
  *            column j (rows j + t) by big_sum, then the columns by big_sum. */
-/* chains per chunk: 64 at d = 64 (pooled_fused64_kernel), 128 above
- * (pooled_fused_big_kernel: one chunk per block iteration, two 64-chain halves) */
-static int64_t orc_big_chunk(int d) { return d == 64 ? 64 : 128; }
+/* chains per chunk: 128 (pooled_fused64_kernel and pooled_fused_big_kernel:
+ * two 64-chain sub-chunks per chunk) */
+static int64_t orc_big_chunk(int d) { (void)d; return 128; }
 
 static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const float* z, const float* pe,
                                  const uint32_t* keys, const float* mu, const float* Lpacked, float lam,

@@ -13,10 +13,10 @@ pytestmark = pytest.mark.gpu
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _bench(args):
+def _bench(args, timeout=110):
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, capture_output=True, text=True,
-                       timeout=110, env=env)
+                       timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout
@@ -29,6 +29,22 @@ def test_bench_two_ranks_one_gpu(gpu):
     assert "configs[4]" in j["config"]["workload"] and "gloo" in j["config"]["parallelism"]
     assert j["pooled"]["chains_total"] == 2 * 8192 and j["pooled"]["sync_every"] == 1
     assert j["value"] > 0 and j["roofline"]["unit"] == "TFLOP/s"
+
+
+@pytest.mark.timeout(600)
+def test_bench_eight_ranks_config5_shape(gpu):
+    """`bench.py --gpus 8` at config 5's own shape (8 x 65,536 chains) on the
+    box's one GPU, every sub-leg included: the weak pooled headline, K = 16,
+    lag-one overlap, the strong-scaling forms over 524,288 chains in total
+    and regime A.  The ranks share the device over
+    gloo, so the numbers are not a scaling measurement."""
+    j = _bench(["--gpus", "8", "--steps", "8", "--warmup", "2"], timeout=540)
+    assert j["n_gpus"] == 8 and "gloo" in j["config"]["parallelism"]
+    assert j["pooled"]["chains_total"] == 8 * 65536 and j["pooled"]["chains_per_gpu"] == 65536
+    for leg in ("pooled_sync_every_16", "pooled_overlap", "strong_pooled", "strong_pooled_sync_every_16", "regime_a"):
+        assert leg in j and j[leg]["value"] > 0, leg
+    assert j["strong_pooled"]["chains_total"] == 524288 and j["strong_pooled"]["chains_per_gpu"] == 65536
+    assert j["strong_pooled_sync_every_16"]["sync_every"] == 16
 
 
 def test_bench_one_gpu_headline(gpu):

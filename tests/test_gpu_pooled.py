@@ -239,9 +239,9 @@ def test_config5_eight_ranks_full_shape(steps, K, gpu, tmp_path):
     test_pooled_two_ranks(64, 524288, steps, K, False, 8, gpu, tmp_path)
 
 
-@pytest.mark.parametrize("d,C", [(128, 700), (256, 300)])
+@pytest.mark.parametrize("d,C", [(64, 3000), (128, 700), (256, 300)])
 def test_pooled_noise_ahead_invalidation(d, C, gpu, orc):
-    """Above d = 64 the update launch draws the next step's noise ahead of
+    """From d = 64 up the update launch draws the next step's noise ahead of
     time; each chain's record (i, key) decides whether the stats kernel may
     use it.  Editing the keys or the counter between steps must fall back to
     drawing, bit for bit against the oracle."""
