@@ -56,11 +56,25 @@ def pooled_flops_per_chain_step(d: int) -> int:
     return 2 * (d * (d + 1) // 2 + d * d + d * (d + 1) // 2)
 
 
-def ess_of(x: np.ndarray) -> float:
-    """Multi-chain ESS of x [chains, draws] (numpyro's estimator, the n_eff
-    of print_summary: adaptive-mcmc_amd/infer_amd/diagnostics.py)."""
+def ess_of(x):
+    """Multi-chain ESS of x [chains, draws, ...] (numpyro's estimator, the n_eff
+    of print_summary: adaptive-mcmc_amd/infer_amd/diagnostics.py; a device
+    tensor is reduced on the device)."""
     from infer_amd.diagnostics import effective_sample_size
-    return float(effective_sample_size(x))
+    return np.atleast_1d(effective_sample_size(x))
+
+
+def cpu_model() -> str:
+    """`lscpu` model name of this host (BASELINE.md §2 asks for it)."""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
 
 
 def measured_traffic(C: int, d: int):
@@ -291,31 +305,35 @@ def pooled_line(ctx, r, total, d, C):
             "collective": coll, "clock_warm": r["clock_warm"]}
 
 
-def ess_leg(ctx, g, burn_in=20000, T=1000, Cs=4096):
-    """ESS/s after a stated per-chain adaptation: Cs chains adapt for burn_in
-    steps (fused launches), then T recorded steps; ESS over 4 coordinates + U."""
+def ess_leg(k, st, burn_in=20000, T=1000):
+    """ESS/s of the headline's own chains (all of them): after the timed region
+    they adapt for `burn_in` more steps (fused launches), then T recorded
+    transitions in one fused launch that collects z and U on the device; ESS
+    (numpyro's multi-chain estimator, reduced on the device) over 4
+    coordinates + U, the minimum reported; ESS/s = that / the recorded
+    launch's wall time."""
     import torch
-    from kernels_amd import ARWMH, PRNGKey
-    d = g.dim
-    ks = ARWMH(potential_fn=g, num_chains=Cs, device=ctx.dev)
-    gen = torch.Generator(device=ctx.dev)
-    gen.manual_seed(7)
-    zs = (torch.rand(Cs, d, device=ctx.dev, generator=gen) * 4.0 - 2.0).contiguous()
-    ss = ks.init(PRNGKey(1), 0, zs, (), {})
+    d = st.z.shape[1]
+    C = st.z.shape[0]
+    i0 = int(st.i[0])
     for _ in range(burn_in // 1000):
-        ks.sample_(ss, 1000)
+        k.sample_(st, 1000)
     torch.cuda.synchronize()
-    acc_burn = float(ss.mean_accept_prob.mean())
+    acc_burn = float(st.mean_accept_prob.mean())
     e0 = time.perf_counter()
-    ss, cz, cp = ks.run(ss, T, collect_z=True, collect_pe=True)
+    st2, cz, cp = k.run(st, T, collect_z=True, collect_pe=True)
     torch.cuda.synchronize()
     el = time.perf_counter() - e0
-    zc, pc = cz.cpu().numpy(), cp.cpu().numpy()
-    vals = [ess_of(zc[:, :, j].T.astype(np.float64)) for j in (0, 1, d // 2, d - 1)]
-    vals.append(ess_of(pc.T.astype(np.float64)))
-    return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": Cs, "draws": T, "seconds": el,
-            "burn_in": burn_in, "mean_accept_prob_after_burn_in": acc_burn,
-            "mean_accept_prob_window": float(ss.mean_accept_prob.mean()), "coords": [0, 1, d // 2, d - 1, "U"]}
+    coords = [0, 1, d // 2, d - 1]
+    x = cz[:, :, coords].permute(1, 0, 2)  # [C, T, 4]
+    vals = [float(v) for v in ess_of(x)]
+    del x, cz
+    vals.append(float(ess_of(cp.t())))
+    return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": C, "draws": T, "seconds": el,
+            "chains_source": "the headline run's own chains, continued after its timed region",
+            "burn_in": burn_in, "steps_before_burn_in": i0, "mean_accept_prob_after_burn_in": acc_burn,
+            "mean_accept_prob_window": float(st2.mean_accept_prob.mean()), "coords": coords + ["U"],
+            "ess_per_coord": vals}
 
 
 def cpu_baseline(g, d: int, budget_s: float = 12.0):
@@ -339,7 +357,281 @@ def cpu_baseline(g, d: int, budget_s: float = 12.0):
         if el >= budget_s or el / steps * (steps + 1) > 2.5 * budget_s:
             break
     return {"value": C * steps / el, "unit": "chain-steps/s", "cores": orc.num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
             "sample": f"C oracle (oracle/amh_oracle.c), {C} chains x {steps} steps, d={d}, {el:.1f} s"}
+
+
+# ------------------------------------------------------- per-config lines --
+# `bench.py --configs [names]`: one JSON line per BASELINE.json single-GPU
+# configuration that is not the headline (BASELINE.md §2 asks, per config, for
+# GPU and CPU chain-steps/s, the speed-up, ESS/s and the roofline).  Synthetic
+# data of the reference shapes.
+CONFIG_NAMES = ("diamonds", "diamonds_ss", "gauss256", "gauss256_pooled", "gauss256_pooled_k16", "pooled64",
+                "pooled64_k16", "asss64", "asss_es", "pnx")
+DIAMONDS_FLOPS = 2 * 5000 * 24 + 20000  # contraction + residual terms per chain-step
+
+
+def cpu_bounded(make_step, C_full: int, budget_s: float = 6.0, label: str = ""):
+    """CPU baseline of one config: the C oracle (test infrastructure, OpenMP
+    over chains) on a bounded sample -- a chain subset sized so that a step
+    takes about a third of the budget, as many whole steps as fit."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    n = min(C_full, 512)
+    step = make_step(n)
+    step()
+    t0 = time.perf_counter()
+    step()
+    el = max(time.perf_counter() - t0, 1e-6)
+    n = int(min(C_full, max(n, n * (budget_s / 3.0) / el)))
+    step = make_step(n)
+    steps, t0 = 0, time.perf_counter()
+    while True:
+        step()
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s or el / steps * (steps + 1) > 2.0 * budget_s:
+            break
+    return {"value": n * steps / el, "unit": "chain-steps/s", "cores": orc.num_threads(), "kind": "port",
+            "cpu_model": cpu_model(),
+            "sample": f"C oracle{label}: {n} of the config's {C_full} chains x {steps} steps, {el:.1f} s"}
+
+
+def _orc_model(kind, obj, data=None):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    import posteriors as P
+    if kind == "gaussian":
+        arr, _ = obj.pack("cpu")
+        return orc.Model(orc.GAUSSIAN, obj.dim, arr.numpy())
+    arr, ip = obj.pack_fn(data)
+    if obj is P.eight_schools:
+        return orc.Model(orc.EIGHT_SCHOOLS, ip[0] + 2, arr)
+    mid = orc.DIAMONDS if obj is P.diamonds else orc.DIAMONDS_SS
+    return orc.Model(mid, ip[1] + 1, arr, n_data=ip[0], k_data=ip[1])
+
+
+def cpu_regime_a(om, C_full, asss=False):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    from kernels_amd import PRNGKey
+
+    def make(n):
+        z0 = np.random.default_rng(0).uniform(-2, 2, size=(n, om.d)).astype(np.float32)
+        st = orc.init(om, PRNGKey(0), n, init_z=z0)
+        return (lambda: orc.asss_step(om, st, 1)) if asss else (lambda: orc.step(om, st, 1))
+    return cpu_bounded(make, C_full, label=" (ASSS)" if asss else "")
+
+
+def cpu_pooled(om, C_full, K=1):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import orc
+    from kernels_amd import PRNGKey
+
+    def make(n):
+        z = np.random.default_rng(0).uniform(-2, 2, size=(n, om.d)).astype(np.float32)
+        box = {"z": z, "pe": orc.potential(om, z), "sh": orc.pooled_init_shared(om.d)}
+        keys = orc.chain_keys(PRNGKey(0), 0, n)
+
+        def step():
+            sh = box["sh"]
+            box["z"], box["pe"], sums = orc.pooled_stats(om, int(sh["i"][0]), box["z"], box["pe"], keys, sh["mu"],
+                                                         sh["L"], float(sh["lam"][0]), k_steps=K)
+            orc.pooled_update(om, sums, sh, k_steps=K)
+        return step
+    r = cpu_bounded(make, C_full, label=" (pooled stats + update)")
+    if K > 1:
+        r["value"] *= K  # one call = K transitions of every chain
+    return r
+
+
+def ess_window(kernel, st, T, coords, every=1):
+    """ESS over `coords` + U of T recorded draws (one fused run() launch with
+    on-device collection), reduced on the device; ESS/s over that launch."""
+    import torch
+    torch.cuda.synchronize()
+    e0 = time.perf_counter()
+    st2, cz, cp = kernel.run(st, T * every, thinning=every, collect_z=True, collect_pe=True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - e0
+    vals = [float(ess_of(cz[:, :, j].t())[0]) for j in coords]
+    vals.append(float(ess_of(cp.t())[0]))
+    del cz, cp
+    return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": st.z.shape[0], "draws": T,
+            "thinning": every, "seconds": el, "coords": list(coords) + ["U"], "ess_per_coord": vals}
+
+
+def _timed_events(fn, steps, stream):
+    import torch
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(steps):
+        fn()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, ev0.elapsed_time(ev1) / steps
+
+
+def config_regime_a(name, kernel, C, d, kwargs, steps, dev, om, roof, ess_burn=0, asss=False, cpu=True):
+    """sample() per launch (one transition of every chain, state round trip
+    through HBM), after a 0.3 s clock warm-up; then the fused rate, the CPU
+    baseline and (ess_burn > 0) ESS/s after ess_burn fused adaptation steps."""
+    import torch
+    from kernels_amd import PRNGKey
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = kernel.init(PRNGKey(0), 0, z0, (), kwargs)
+    warm = clock_warm(lambda: kernel.sample_(st, 1), _SoloCtx())
+    wall, kms = _timed_events(lambda: kernel.sample_(st, 1), steps, torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    f0 = time.perf_counter()
+    kernel.sample_(st, 10)
+    torch.cuda.synchronize()
+    fused = C * 10 / (time.perf_counter() - f0)
+    rate = C * steps / wall
+    line = {"config": name, "chains": C, "dim": d, "steps": steps, "value": rate, "unit": "chain-steps/s",
+            "kernel_ms": kms, "fused_chain_steps_per_s": fused, "clock_warm": warm,
+            "mean_accept_prob": float(st.mean_accept_prob.mean()) if hasattr(st, "mean_accept_prob") else None}
+    if roof == "hbm":
+        b = C * bytes_per_chain_step(d)
+        line["roofline"] = {"bound": "hbm", "achieved": b / (kms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": b / (kms * 1e-3) / 1e9 / HBM_PEAK_GBS, "algorithmic_bytes_per_step": b}
+    elif roof == "fp32":
+        fl = C * DIAMONDS_FLOPS
+        line["roofline"] = {"bound": "mfma", "achieved": fl / (kms * 1e-3) / 1e12, "peak": FP32_PEAK_TFLOPS,
+                            "unit": "TFLOP/s", "frac": fl / (kms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS,
+                            "algorithmic_flops_per_step": fl, "over": "the whole transition (all its launches)"}
+    if ess_burn:
+        for _ in range(ess_burn // 1000):
+            kernel.sample_(st, 1000)
+        torch.cuda.synchronize()
+        line["ess"] = ess_window(kernel, st, 1000, [0, 1, d // 2, d - 1])
+        line["ess"]["burn_in"] = ess_burn
+        line["ess"]["mean_accept_prob_after_burn_in"] = line["mean_accept_prob"] = (
+            float(st.mean_accept_prob.mean()) if hasattr(st, "mean_accept_prob") else None)
+    if cpu:
+        line["cpu_baseline"] = cpu_regime_a(om, C, asss=asss)
+        line["speedup_vs_cpu"] = rate / line["cpu_baseline"]["value"]
+    return line
+
+
+class _SoloCtx:
+    """Ctx stand-in for the single-process per-config runs."""
+    world = 1
+
+    def barrier(self):
+        pass
+
+    def max_over_ranks(self, x):
+        return float(x)
+
+
+def config_pooled(key, d, C, kappa, K, steps, dev, burn_in, ess=True, cpu=True):
+    import torch
+    import posteriors as P
+    from kernels_amd import PooledARWMH, PRNGKey
+    g = P.correlated_gaussian(d, log10_kappa=kappa)
+    k = PooledARWMH(potential_fn=g, num_chains=C, device=dev, sync_every=K)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(9)
+    z0 = (torch.rand(C, d, device=dev, generator=gen) * 4.0 - 2.0).contiguous()
+    st = k.init(PRNGKey(0), 0, z0, (), {})
+    burn_in = -(-burn_in // K) * K
+    k.sample_(st, burn_in)
+    torch.cuda.synchronize()
+    macc_burn = float(st.mean_accept_prob[0])
+    warm = clock_warm(lambda: k.sample_(st, K), _SoloCtx())
+    nb = -(-steps // K)
+    wall, kms = _timed_events(lambda: k.sample_(st, K), nb, torch.cuda.current_stream(dev))
+    fl = pooled_flops_per_chain_step(d)
+    rate = C * nb * K / wall
+    sms = pooled_stats_ms(k, st, C) / K
+    line = {"config": f"{key} regime B" + (f", sync_every={K}" if K > 1 else ""), "chains": C, "dim": d,
+            "steps": nb * K, "value": rate, "unit": "chain-steps/s", "ms_per_step": kms / K, "burn_in": burn_in,
+            "mean_accept_prob_after_burn_in": macc_burn, "mean_accept_prob": float(st.mean_accept_prob[0]),
+            "clock_warm": warm,
+            "roofline": {"bound": "mfma", "achieved": rate * fl / 1e12, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": rate * fl / 1e12 / FP32_PEAK_TFLOPS, "over": "the whole step",
+                         "flops_per_chain_step": fl, "stats_kernel_ms": sms,
+                         "stats_kernel_frac": C * fl / (sms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
+    if ess and K == 1:
+        line["ess"] = ess_window(k, st, 1000, [0, 1, d // 2, d - 1])
+    if cpu:
+        line["cpu_baseline"] = cpu_pooled(_orc_model("gaussian", g), C, K)
+        line["speedup_vs_cpu"] = rate / line["cpu_baseline"]["value"]
+    return line
+
+
+def configs_main(names, steps):
+    import torch
+    import posteriors as P
+    from kernels_amd import ARWMH, ASSS, PRNGKey
+    want = set(names)
+    bad = want - set(CONFIG_NAMES)
+    if bad:
+        raise SystemExit(f"bench.py --configs: unknown {sorted(bad)}; known {CONFIG_NAMES}")
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py: no GPU visible")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+
+    def emit(line):
+        print(json.dumps(line), flush=True)
+    if "diamonds" in want:
+        data = P.synthetic_diamonds()
+        k = ARWMH(model=P.diamonds, num_chains=262144, device=dev)
+        emit(config_regime_a("diamonds, literal per-row likelihood (BASELINE configs[2])", k, 262144,
+                             P.diamonds.dim(data), data, steps, dev, _orc_model("m", P.diamonds, data), "fp32"))
+    if "diamonds_ss" in want:
+        data = P.synthetic_diamonds()
+        k = ARWMH(model=P.diamonds_suffstat, num_chains=262144, device=dev)
+        emit(config_regime_a("diamonds, sufficient-statistics likelihood (BASELINE configs[2])", k, 262144,
+                             P.diamonds_suffstat.dim(data), data, steps, dev,
+                             _orc_model("m", P.diamonds_suffstat, data), "hbm", ess_burn=20000))
+    if "gauss256" in want:
+        g = P.correlated_gaussian(256, log10_kappa=4.0)
+        k = ARWMH(potential_fn=g, num_chains=32768, device=dev)
+        emit(config_regime_a("gauss256 regime A, kappa=1e4 (BASELINE configs[3])", k, 32768, 256, {}, steps, dev,
+                             _orc_model("gaussian", g), "hbm"))
+    if "asss64" in want:
+        g = P.correlated_gaussian(64)
+        k = ASSS(potential_fn=g, num_chains=65536, device=dev)
+        emit(config_regime_a("ASSS d=64 correlated Gaussian", k, 65536, 64, {}, steps, dev, _orc_model("gaussian", g),
+                             "hbm", asss=True))
+    if "asss_es" in want:
+        data = dict(P.EIGHT_SCHOOLS_DATA)
+        k = ASSS(model=P.eight_schools, num_chains=262144, device=dev)
+        emit(config_regime_a("ASSS eight schools", k, 262144, 10, data, steps, dev,
+                             _orc_model("m", P.eight_schools, data), None, asss=True))
+    for key, d, C, kappa, K, burn in (("gauss256_pooled", 256, 32768, 4.0, 1, 4096),
+                                      ("gauss256_pooled_k16", 256, 32768, 4.0, 16, 4096),
+                                      ("pooled64", 64, 65536, 2.0, 1, 256), ("pooled64_k16", 64, 65536, 2.0, 16, 4096)):
+        if key in want:
+            emit(config_pooled(key.replace("_k16", ""), d, C, kappa, K, max(steps, 32), dev, burn))
+    if "pnx" in want:
+        # many-chain frozen kernel (sample_Pnx, the Lipschitz sweeps' sampler):
+        # 5e4 start points x 1e3 chains each x 1 step, eight schools
+        data = dict(P.EIGHT_SCHOOLS_DATA)
+        for Kc in (ARWMH, ASSS):
+            k = Kc(model=P.eight_schools, num_chains=64, device=dev)
+            st = k.init(PRNGKey(0), 0, None, (), data)
+            k.sample_(st, 2000)
+            x = st.z[:50].repeat(1000, 1).contiguous()  # 5e4 points
+            adapt = st.adapt_state
+            shared = (adapt.loc[0], adapt.scale[0]) + ((adapt.log_step_size[0],) if Kc is ARWMH else ())
+            k.sample_Pnx(PRNGKey(1), x, shared, n=1, n_samples=1000)  # warm
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            reps = 5
+            for r in range(reps):
+                k.sample_Pnx(PRNGKey(2 + r), x, shared, n=1, n_samples=1000)
+            torch.cuda.synchronize()
+            wall = time.perf_counter() - t0
+            emit({"config": f"{Kc.__name__}.sample_Pnx eight schools", "chains": 50000 * 1000, "dim": 10, "steps": 1,
+                  "value": reps * 5e7 / wall, "unit": "chain-steps/s", "ms_per_call": wall / reps * 1e3})
 
 
 # ------------------------------------------------------------------- main --
@@ -355,7 +647,13 @@ def main():
     ap.add_argument("--no-pooled", action="store_true", help="N = 1: skip the pooled sub-fields")
     ap.add_argument("--no-extra", action="store_true", help="headline leg only (profiling runs)")
     ap.add_argument("--no-fused", action="store_true", help="skip the fused 50-step launch (profiling runs)")
+    ap.add_argument("--configs", nargs="?", const=",".join(CONFIG_NAMES), default=None,
+                    help="per-config lines instead of the headline (comma list; default all): " + ",".join(CONFIG_NAMES))
     args = ap.parse_args()
+    if args.configs is not None:
+        if args.gpus != 1:
+            raise SystemExit("--configs runs on one GPU")
+        return configs_main(args.configs.split(","), args.steps if args.steps != 200 else 20)
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
@@ -400,7 +698,7 @@ def main():
                                 ("pooled_overlap", 1, True)):
                 pr = leg_pooled(ctx, g, C, 0, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
                 sub[name] = pooled_line(ctx, pr, C, d, C)
-        ess = ess_leg(ctx, g) if extra and not args.no_ess else None
+        ess = ess_leg(r["kernel"], r["state"]) if extra and not args.no_ess else None
         cpu = cpu_baseline(g, d) if extra and not args.no_cpu_baseline else None
         line = {"metric": metric, "value": value, "unit": "chain-steps/s", "n_gpus": 1, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": r["wall"] / args.steps * 1e3, "higher_is_better": True,

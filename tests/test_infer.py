@@ -44,6 +44,21 @@ def test_ess_matches_direct_sum(C, N):
     assert np.allclose(D.effective_sample_size(x), _ess_direct(x), rtol=1e-9)
 
 
+@pytest.mark.parametrize("shape", [(1, 200), (4, 101), (3, 64), (6, 150, 3)])
+def test_ess_torch_path_matches_numpy(shape):
+    # bench.py hands device tensors (65,536 chains x 1,000 draws) to the torch
+    # restatement; on CPU tensors it must agree with the numpy path
+    import torch
+    rng = np.random.default_rng(sum(shape))
+    x = _ar1(rng, shape[0] * (shape[2] if len(shape) > 2 else 1), shape[1], 0.5)
+    if len(shape) > 2:
+        x = x.reshape(shape[0], shape[2], shape[1]).transpose(0, 2, 1).copy()
+    got = D.effective_sample_size(torch.as_tensor(x))
+    assert np.allclose(got, D.effective_sample_size(x), rtol=1e-10)
+    with pytest.raises(ValueError):
+        D.effective_sample_size(torch.zeros(3, 1))
+
+
 def test_ess_ar1_closed_form():
     # tau = (1 + phi) / (1 - phi) for an AR(1) chain
     phi = 0.8

@@ -8,6 +8,6 @@ rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed" gpurun_out/pytest_gpu.log |
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_full.log 2>&1
 rc=$?; echo "bench rc=$rc"; grep -v amdgpu.ids gpurun_out/bench_full.log | tail -2
 [ $rc -eq 0 ] || exit $rc
-timeout -k 10 300 python -u tools/bench_configs.py --steps 20 > gpurun_out/cfg.log 2>&1
+timeout -k 10 300 python -u bench.py --configs --steps 20 > gpurun_out/cfg.log 2>&1
 rc=$?; echo "configs rc=$rc"; grep config gpurun_out/cfg.log
 exit $rc
