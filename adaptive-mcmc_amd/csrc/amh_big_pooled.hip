@@ -429,6 +429,9 @@ template <int NT>
 constexpr size_t fused_big_lds_bytes() {
   return ((size_t)2 * 32 * NT * kLd + (size_t)NT * 64 + 3 * 64 + 32 * NT) * sizeof(float);
 }
+__host__ __device__ constexpr int64_t pooled_big_tile_V_dev(int d) {
+  return d + (int64_t)((d / 32) * (d / 32 + 1) / 2) * 1024 + 4;
+}
 int64_t pooled_big_tile_V(int d) {  // [S_d | S_dd tiles | 2 pad | S_a | N]: a multiple of 4
   const int nt = d / 32;
   return d + (int64_t)(nt * (nt + 1) / 2) * 1024 + 4;
@@ -1186,6 +1189,137 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
 // the panel kernel it replaces and of orc_pooled_update_big).  The write-out
 // and as_change (column sums by the 64-lane butterfly, then the columns)
 // follow on all four waves.
+// ------------------------------------------------ d = 64 chunk reduction --
+// The fused d = 64 kernel's float32 partial rows (tile layout, V floats per
+// 128-chain chunk) -> the packed double sums, in the bit spec's order
+// (pooled_group4_kernel + pooled_final_kernel): per entry, the chunks of each
+// group of 16 summed in chunk order from 0.0, then the group sums in group
+// order from 0.0 (then += the sums so far when accumulating over a pooled
+// block).  One 512-thread block owns 16 float4 columns of the row for every
+// group: thread (tg, c) sums group 32 gt + tg of column c into LDS, then 64
+// threads (column, component) add the 32 group sums in order, tile by tile.
+// One launch instead of two; with `coherent` the sums go out write-through
+// (agent-scope stores) for a reader in another XCD.
+constexpr int kRedCols = 16;  // float4 columns per reduce block
+constexpr int kRedGrp = 16;   // chunks per group (pooled_reduce's kRedGroup)
+int pooled_reduce64_blocks(int64_t V) { return (int)((V / 4 + kRedCols - 1) / kRedCols); }
+
+__device__ __forceinline__ void reduce64_slice(const float* __restrict__ partials, int64_t n_chunks, int64_t V,
+                                               double* sums, int accumulate, int blk, bool coherent) {
+  __shared__ double gs[32][kRedCols][4];
+  const int tid = threadIdx.x;
+  const int c = tid & (kRedCols - 1), tg = tid >> 4;  // 512 threads: 16 columns x 32 groups
+  const int64_t v4 = (int64_t)blk * kRedCols + c;
+  const bool col_ok = 4 * v4 < V;
+  const int64_t n_groups = (n_chunks + kRedGrp - 1) / kRedGrp;
+  const int fc = tid >> 2, comp = tid & 3;  // finishing threads (tid < 64)
+  double tot = 0.0;
+  for (int64_t g0 = 0; g0 < n_groups; g0 += 32) {
+    const int64_t g = g0 + tg;
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    if (g < n_groups && col_ok) {
+      const int64_t q0 = g * kRedGrp;
+      const int64_t q1 = q0 + kRedGrp < n_chunks ? q0 + kRedGrp : n_chunks;
+      float4 x[kRedGrp];
+#pragma unroll
+      for (int q = 0; q < kRedGrp; ++q) x[q] = (q0 + q < q1) ? ((const float4*)(partials + (q0 + q) * V))[v4] : float4{};
+#pragma unroll
+      for (int q = 0; q < kRedGrp; ++q)
+        if (q0 + q < q1) {  // chunk order; a missing tail chunk is not added at all
+          s0 += (double)x[q].x;
+          s1 += (double)x[q].y;
+          s2 += (double)x[q].z;
+          s3 += (double)x[q].w;
+        }
+    }
+    gs[tg][c][0] = s0;
+    gs[tg][c][1] = s1;
+    gs[tg][c][2] = s2;
+    gs[tg][c][3] = s3;
+    __syncthreads();
+    if (tid < 64) {
+      const int64_t ng = n_groups - g0 < 32 ? n_groups - g0 : 32;
+      for (int q = 0; q < ng; ++q) tot += gs[q][fc][comp];  // group order
+    }
+    __syncthreads();
+  }
+  if (tid < 64) {
+    const int64_t u = 4 * ((int64_t)blk * kRedCols + fc) + comp;
+    const int64_t v = u < V ? tile_to_packed(u, V, kF) : -1;
+    if (v >= 0) {
+      const double sv = accumulate ? sums[v] + tot : tot;
+      if (coherent) {
+        __hip_atomic_store(&sums[v], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        sums[v] = sv;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void pooled_reduce64_kernel(const float* __restrict__ partials, int64_t n_chunks,
+                                                              int64_t V, double* sums, int accumulate) {
+  reduce64_slice(partials, n_chunks, V, sums, accumulate, (int)blockIdx.x, false);
+}
+
+// sqrtf(x) and then n / sqrtf(x), spelled out as the compiler's IEEE
+// expansions for gfx950 with f32 denormals on (v_sqrt_f32 + the +-1 ulp
+// residual correction, 2^32 pre-scaling below 2^-96, the zero/+inf class
+// select; v_div_scale / v_rcp / Newton fmas / v_div_fmas / v_div_fixup) --
+// the same instructions in the same order, so the same bits as `sqrtf` and
+// `/` (the oracle's operations).  fill(S), S = 0..15, runs after step S with a
+// scheduling barrier on both sides: independent work placed in the chain's
+// dependency stalls (an in-order wave cannot reorder it there by itself, and
+// the compiler's scheduler does not).
+template <class F>
+__device__ __forceinline__ void ieee_sqrt_div(float x0, float n, float& sq, float& qt, F&& fill) {
+  using I = std::integral_constant<int, 0>;
+  auto step = [&](auto S) {
+    __builtin_amdgcn_sched_barrier(0);
+    fill(S);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const bool sc = x0 < 0x1p-96f;
+  const float x = sc ? x0 * 0x1p32f : x0;
+  step(std::integral_constant<int, 0>{});
+  float r = __builtin_amdgcn_sqrtf(x);
+  step(std::integral_constant<int, 1>{});
+  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
+  step(std::integral_constant<int, 2>{});
+  const float vp = fmaf(-rm, r, x);
+  step(std::integral_constant<int, 3>{});
+  const float vs = fmaf(-rp, r, x);
+  step(std::integral_constant<int, 4>{});
+  r = (vp <= 0.0f) ? rm : r;
+  r = (vs > 0.0f) ? rp : r;
+  step(std::integral_constant<int, 5>{});
+  r = sc ? r * 0x1p-16f : r;
+  const float s = __builtin_amdgcn_classf(x, 0x260) ? x : r;  // +-0, +inf
+  sq = s;
+  step(std::integral_constant<int, 6>{});
+  bool flag = false, unused = false;
+  const float den = __builtin_amdgcn_div_scalef(n, s, false, &unused);
+  const float num = __builtin_amdgcn_div_scalef(n, s, true, &flag);
+  step(std::integral_constant<int, 7>{});
+  const float rc = __builtin_amdgcn_rcpf(den);
+  step(std::integral_constant<int, 8>{});
+  const float f0 = fmaf(-den, rc, 1.0f);
+  step(std::integral_constant<int, 9>{});
+  const float f1 = fmaf(f0, rc, rc);
+  step(std::integral_constant<int, 10>{});
+  const float mu = num * f1;
+  step(std::integral_constant<int, 11>{});
+  const float f2 = fmaf(-den, mu, num);
+  step(std::integral_constant<int, 12>{});
+  const float f3 = fmaf(f2, f1, mu);
+  step(std::integral_constant<int, 13>{});
+  const float f4 = fmaf(-den, f3, num);
+  step(std::integral_constant<int, 14>{});
+  qt = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(f4, f1, f3, flag), s, n);
+  step(std::integral_constant<int, 15>{});
+  (void)sizeof(I);
+}
+
 __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams p) {
   constexpr int d = 64, P = d * (d + 1) / 2, kQ = d / 4;
   constexpr int S = d + 1;  // LDS row stride of the factor
@@ -1193,7 +1327,13 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   __shared__ __attribute__((aligned(16))) float cb[2][64];
   __shared__ float colsum[64];
   __shared__ int okv;
-  if (blockIdx.x > 0) {
+  // wave 0's write-out operands, parked here while it factors (they would
+  // otherwise stay live across the factorisation and spill)
+  __shared__ double park_s[kQ][64], park_c[kQ][64];
+  __shared__ float park_l[kQ][64];
+  const int nred = p.red_blocks;        // > 0: reduce the chunk partials first
+  const int base = nred > 0 ? nred : 1;  // blocks [0, base): reduce / update; the rest draw noise
+  if ((int)blockIdx.x >= base) {
     // extra blocks (one 8-wave block per other CU) beside the single-workgroup
     // update: the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
     // Philox(0, i', 0)[1] of every chain, i' = i + K, each chain's row with
@@ -1202,34 +1342,67 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     const int lane = lane_id();
     // wave wv takes the chains wv, wv + nw, ..; the keys of 32 of them arrive
     // in one vector load (lane l: word l & 1 of the (l >> 1)-th)
-    const int64_t wv = (int64_t)(blockIdx.x - 1) * 8 + threadIdx.x / 64;
-    const int64_t nw = (int64_t)(gridDim.x - 1) * 8;
+    const int64_t wv = (int64_t)(blockIdx.x - base) * 8 + threadIdx.x / 64;
+    const int64_t nw = (int64_t)(gridDim.x - base) * 8;
+    // Four chains per group, straight-line (unrolled rounds, no branch:
+    // a chain past noise_C repeats the last one and does not store), so the
+    // four independent Philox / erfinv chains interleave -- one chain at a
+    // time left the wave waiting on each dependent 64-bit multiply.
     for (int64_t c32 = wv; c32 < p.noise_C; c32 += 32 * nw) {
       int64_t kc = c32 + nw * (lane >> 1);
       if (kc >= p.noise_C) kc = p.noise_C - 1;
       const uint32_t kv = p.keys[2 * kc + (lane & 1)];
-      static_for<32>([&](auto J) {
-        const int64_t ch = c32 + nw * J;
-        if (ch < p.noise_C) {
-          const uint32_t kk0 = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J);
-          const uint32_t kk1 = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J + 1);
-          const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0, kk1);
-          p.xi[ch * d + lane] = amh_normal_from_bits(o.v[0]);
-          const uint32_t ubits = (uint32_t)__builtin_amdgcn_readlane((int)o.v[1], 0);
-          if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0, kk1, ubits);
-        }
-        if constexpr (J % 4 == 3) __builtin_amdgcn_sched_barrier(0);
+      static_for<8>([&](auto G) {
+        if (c32 + nw * (4 * G) >= p.noise_C) return;  // (wave-uniform) no chain of this group left
+        float xv[4];
+        uint32_t kk0[4], kk1[4], ub[4];
+        static_for<4>([&](auto E) {
+          constexpr int J = 4 * G + E;
+          kk0[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J);
+          kk1[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J + 1);
+          const amh_u32x4 o = amh_philox4x32_10_unrolled((uint32_t)lane, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0[E], kk1[E]);
+          xv[E] = amh_normal_from_bits(o.v[0]);
+          ub[E] = (uint32_t)__builtin_amdgcn_readlane((int)o.v[1], 0);
+        });
+        static_for<4>([&](auto E) {
+          const int64_t ch = c32 + nw * (4 * G + E);
+          if (ch < p.noise_C) {
+            p.xi[ch * d + lane] = xv[E];
+            if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0[E], kk1[E], ub[E]);
+          }
+        });
+        __builtin_amdgcn_sched_barrier(0);
       });
     }
     return;
   }
-  if (threadIdx.x >= 256) return;  // block 0: four waves, the CU to themselves
+  const bool coh = nred > 0;  // the sums were just written by other blocks (maybe other XCDs)
+  if (nred > 0) {
+    reduce64_slice(p.red_partials, p.red_chunks, pooled_big_tile_V_dev(d), p.sums_out, p.red_accumulate,
+                   (int)blockIdx.x, true);
+    // the last block to finish its slice runs the update: write-through
+    // stores done (vmcnt(0)), then an agent-scope ticket; the last arriver
+    // reads the sums with agent-scope loads (the cross-XCD hand-off of
+    // pooled_big_post_kernel)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int last;
+    int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
+    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nred - 1;
+    __syncthreads();
+    if (!last) return;
+    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  if (threadIdx.x >= 256) return;  // four waves, the CU to themselves
   if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);  // the factorisation wave first on its SIMD
   const int tid = threadIdx.x;
   US_INIT
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(tid / 64));
   const double* sums = p.sums;
+  auto ldsum = [&](int64_t i) -> double {
+    return coh ? __hip_atomic_load(&sums[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sums[i];
+  };
   // (0) one batch of loads (issued before anything waits on the scalars)
   double sig[kQ], cvo[kQ], sv[kQ];
   float lvo[kQ];
@@ -1237,19 +1410,19 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     const int k = w + 4 * Q;
     const int64_t o = col_off(d, k) + (lane < d - k ? lane : 0);
     cvo[Q] = p.in.cov[o];
-    sv[Q] = sums[d + o];
+    sv[Q] = ldsum(d + o);
     lvo[Q] = p.in.scale[o];
   });
   const float loc_in = p.in.loc[lane];
-  const double sd_in = sums[lane];
-  const double N = sums[d + P + 1];
+  const double sd_in = ldsum(lane);
+  const double N = ldsum(d + P + 1);
   const int32_t it = p.in.i[0];
   const int32_t itr = it + p.K;
   const int32_t n = pooled_block_n(it, p.W, p.K);
   const float gamma = amh_lr_gamma(n, p.a);
   const float macc = p.in.mean_accept_prob[0];
   const float lam = p.in.log_step_size[0];
-  const float abar = (float)(sums[d + P] / N);
+  const float abar = (float)(ldsum(d + P) / N);
   const float maccn = macc + (abar - macc) / (float)n;
   const float lamn = lam + gamma * (abar - p.target);
   // Sigma' in double, rounded into LDS rows
@@ -1261,6 +1434,13 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       const double b = g * (sv[Q] / N);
       sig[Q] = a + b;
       if (lane < d - k) A[(k + lane) * S + k] = (float)sig[Q];
+    });
+  }
+  if (w == 0) {
+    static_for<kQ>([&](auto Q) {
+      park_s[Q][lane] = sig[Q];
+      park_c[Q][lane] = cvo[Q];
+      park_l[Q][lane] = lvo[Q];
     });
   }
   US(0)
@@ -1280,17 +1460,29 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       constexpr int k = K;
       const float piv = rdlane(a[k], k);
       ok = ok && (piv > 0.0f) && amh_isfinite(piv);
-      const float ljj = sqrtf(piv);
-      const float q = a[k] / ljj;
-      __builtin_amdgcn_sched_barrier(0);
-      if constexpr (k >= 1) {  // column k-1's updates of the columns m >= k+1
-        static_for<16>([&](auto Q) {
-          static_for<4>([&](auto E) {
-            constexpr int m = 4 * Q + E;
-            if constexpr (m >= k + 1) a[m] = fmaf(-am1, pv[(int)Q][(int)E], a[m]);
+      // ljj = sqrtf(piv), q = a[k] / ljj as the 16 dependent steps of their
+      // IEEE expansions, each followed by four of column k-1's updates of the
+      // columns m >= k+1 (independent of this chain): the in-order wave
+      // issues those in the chain's latency gaps instead of after it
+      float ljj, q;
+      ieee_sqrt_div(piv, a[k], ljj, q, [&](auto S) {
+        if constexpr (k >= 1) {
+          // packed: two columns (m, m + 1), m even, per v_pk_fma_f32 (an
+          // IEEE fma per element, the same bits as two fmaf); column k + 1
+          // alone when it is odd
+          constexpr int m0 = ((k + 1) % 2 == 0) ? k + 1 : k + 2;
+          if constexpr (S == 0 && m0 != k + 1) a[k + 1] = fmaf(-am1, pv[(k + 1) / 4][(k + 1) % 4], a[k + 1]);
+          static_for<2>([&](auto J) {
+            constexpr int m = m0 + 2 * (2 * S + J);
+            if constexpr (m + 1 < d) {
+              const f32x2v r = __builtin_elementwise_fma(f32x2v{-am1, -am1}, f32x2v{pv[m / 4][m % 4], pv[m / 4][m % 4 + 1]},
+                                                         f32x2v{a[m], a[m + 1]});
+              a[m] = r[0];
+              a[m + 1] = r[1];
+            }
           });
-        });
-      }
+        }
+      });
       a[k] = (ln == k) ? ljj : q;
       if constexpr (k + 1 < d) {
         float* cbk = cb[k & 1];
@@ -1311,6 +1503,14 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   }
   US(2)
   __syncthreads();
+  asm volatile("" ::: "memory");  // the parked values are reloaded, not kept in registers
+  if (w == 0) {
+    static_for<kQ>([&](auto Q) {
+      sig[Q] = park_s[Q][lane];
+      cvo[Q] = park_c[Q][lane];
+      lvo[Q] = park_l[Q][lane];
+    });
+  }
   US(3)
   // (2) write-out and as_change: column k's squared terms (rows k + t) by the
   // 64-lane butterfly, then the columns (pooled_big_post_kernel's order)
@@ -1463,7 +1663,11 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     (void)V;
-    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d);
+    if (p.defer_reduce) return hipSuccess;  // the update launch reduces (run_pooled_big_update)
+    const int64_t Vt = pooled_big_tile_V(d);
+    hipLaunchKernelGGL(pooled_reduce64_kernel, dim3((unsigned)pooled_reduce64_blocks(Vt)), dim3(512), 0, s,
+                       (const float*)p.partials, nch, Vt, sums, p.accumulate);
+    return hipGetLastError();
   }
   {
     const int nt = d / 32;
@@ -1505,12 +1709,16 @@ hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, boo
     if (e != hipSuccess) return e;
   }
   if (p.d == 64) {
-    unsigned nb = 1;  // + one noise block per other CU when the next step's noise is drawn ahead
+    // blocks: the reduce blocks (red_blocks > 0; the last to finish runs the
+    // update) or the one update block, then noise blocks up to one per CU
+    // when the next step's noise is drawn ahead
+    const unsigned head = p.red_blocks > 0 ? (unsigned)p.red_blocks : 1u;
+    unsigned nb = head;
     if (p.noise_C > 0 && p.xi != nullptr) {
       int dev = 0, cus = 0;
       (void)hipGetDevice(&dev);
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      nb = (unsigned)(cus > 1 ? cus : 2);
+      nb = (unsigned)cus > head + 1 ? (unsigned)cus : head + 1;
     }
     hipLaunchKernelGGL(pooled_update64_kernel, dim3(nb), dim3(512), 0, s, p);
     return hipGetLastError();

@@ -532,10 +532,30 @@ int amh_pooled_sums_size(int32_t dim, int64_t* v) {
 // prep_for_update: the update follows in the same library call with no
 // exchange in between (amh_pooled_step_k on one rank), so the large-d
 // reduction's last kernel also forms that update's Sigma'
+// AMH_POOLED_FUSED_REDUCE=0: keep the d = 64 reduction in its own launch
+// (A/B switch; the bits are the same either way)
+static bool reduce_fusion_off() {
+  static const bool off = [] {
+    const char* e = getenv("AMH_POOLED_FUSED_REDUCE");
+    return e != nullptr && e[0] == '0';
+  }();
+  return off;
+}
+
+// d = 64 with prep_for_update: the last step's chunk partials are left
+// unreduced; *deferred describes them for the update launch, which reduces
+// them first (one launch fewer per pooled block)
+struct DeferredReduce {
+  const float* partials = nullptr;
+  int64_t n_chunks = 0;
+  int32_t accumulate = 0;
+};
+
 static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
                              float* z_out, float* pe_out, double* sums, void* stream, bool prep_for_update,
-                             bool* sigma_ready) {
+                             bool* sigma_ready, DeferredReduce* deferred = nullptr) {
   if (sigma_ready) *sigma_ready = false;
+  if (deferred) *deferred = DeferredReduce{};
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_stats: null handle");
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
   if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1 || k_steps < 1)
@@ -627,6 +647,12 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
         p.z = z_out;
         p.pe = pe_out;
       }
+      p.defer_reduce = (prep_for_update && deferred && d == 64 && t == k_steps - 1 && !reduce_fusion_off()) ? 1 : 0;
+      if (p.defer_reduce) {
+        deferred->partials = (const float*)h->partials;
+        deferred->n_chunks = n_chunks;
+        deferred->accumulate = p.accumulate;
+      }
       e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
                                     (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(MFMA path)");
@@ -639,7 +665,8 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
 }
 
 static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
-                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready);
+                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready,
+                              const DeferredReduce* deferred = nullptr);
 
 extern "C" {
 
@@ -661,7 +688,8 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
 }  // extern "C"
 
 static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
-                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready) {
+                              const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready,
+                              const DeferredReduce* deferred) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_update: null handle");
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
   if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
@@ -693,6 +721,13 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
       p.xrec = (uint4*)h->noise_buf;
       p.xi = h->noise_buf + 4 * h->noise_cap;
     }
+    if (deferred && deferred->partials) {
+      p.red_partials = deferred->partials;
+      p.red_chunks = deferred->n_chunks;
+      p.red_accumulate = deferred->accumulate;
+      p.red_blocks = amh::pooled_reduce64_blocks(amh::pooled_big_tile_V(p.d));
+      p.sums_out = const_cast<double*>(sums);
+    }
     e = amh::run_pooled_big_update(p, (hipStream_t)stream, sigma_ready);
   } else {
     e = amh::run_pooled_update(p, (hipStream_t)stream);
@@ -715,10 +750,11 @@ int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state*
   const amh_pooled_state* src = in;
   for (int32_t t = 0; t < n_steps; t += sync_every) {
     bool ready = false;  // one rank, no exchange: the reduction also forms Sigma'
+    DeferredReduce dr;   // (d = 64: or is left to the update launch)
     int rc = pooled_stats_impl(h, num_chains, src, sync_every, out->z, out->potential_energy, sums, stream, true,
-                               &ready);
+                               &ready, &dr);
     if (rc != AMH_OK) return rc;
-    rc = pooled_update_impl(h, sums, src, out, sync_every, stream, ready);
+    rc = pooled_update_impl(h, sums, src, out, sync_every, stream, ready, &dr);
     if (rc != AMH_OK) return rc;
     src = out;
   }

@@ -120,6 +120,9 @@ struct PooledStatsParams {
   const uint4* xrec;
   int64_t xi_cap;
   FinalPrep prep;  // scratch == nullptr: none
+  // d = 64: the chunk partials are left for the update launch to reduce
+  // (amh_pooled_step_k on one rank: the update follows with no exchange)
+  int32_t defer_reduce;
 };
 
 // Pool-every-K: the update after a block of K transitions that started at
@@ -142,7 +145,15 @@ struct PooledUpdateParams {
   const uint32_t* keys;
   float* xi;
   uint4* xrec;
+  // d = 64, red_blocks > 0: the launch first reduces the stats launch's chunk
+  // partials into sums_out (== sums; the last reduce block to finish runs
+  // the update)
+  const float* red_partials;
+  int64_t red_chunks;
+  int32_t red_accumulate, red_blocks;
+  double* sums_out;
 };
+int pooled_reduce64_blocks(int64_t V);  // reduce blocks of the d = 64 partial rows
 
 hipError_t run_pooled_stats(int model_id, const PooledStatsParams& p, double* sums, hipStream_t s);
 // large dimensions (amh_big_pooled.hip): chunks of 256 chains

@@ -273,27 +273,6 @@ __global__ __launch_bounds__(256) void pooled_group4_kernel(const float* __restr
   o[3] = s3;
 }
 
-// Row u of a "tile" partial (pooled_fused_big_kernel, d > 64): [d S_d | NPAIR
-// 32x32 tiles of S_dd in MFMA register order (pair, reg R, lane) | S_a | N]
-// -> its index in the packed sums vector (-1: above the diagonal of a
-// diagonal tile, not part of the sums).
-__device__ int64_t tile_to_packed(int64_t u, int64_t Vt, int d, int* prow = nullptr, int* pcol = nullptr) {
-  const int64_t P = (int64_t)d * (d + 1) / 2;
-  if (u < d) return u;
-  if (u >= Vt - 2) return u - Vt + d + P + 2;
-  if (u >= Vt - 4) return -1;  // padding (V % 4 == 0)
-  const int64_t q = u - d;
-  const int pair = (int)(q >> 10), R = (int)((q >> 6) & 15), lane = (int)(q & 63);
-  int I = 0;
-  while ((I + 1) * (I + 2) / 2 <= pair) ++I;
-  const int J = pair - I * (I + 1) / 2;
-  const int row = 32 * I + (R & 3) + 8 * (R >> 2) + 4 * (lane >> 5), col = 32 * J + (lane & 31);
-  if (row < col) return -1;
-  if (prow) *prow = row;
-  if (pcol) *pcol = col;
-  return d + (int64_t)col * d - (int64_t)col * (col - 1) / 2 + (row - col);
-}
-
 // the update's 4-row-aligned layout (amh_big_pooled.hip a4_base)
 __device__ __forceinline__ int fp_a4_base(int d, int j) {
   const int q = j >> 2;

@@ -107,6 +107,15 @@ def _pair_mask(X: torch.Tensor):
     return dists, (lower <= dists) & (dists <= upper)
 
 
+def _init_seed(rng_key) -> int:
+    """The network's initialisation follows the key like flax's
+    model.init(rng_key, ..) (lipschitz.py:137-139, :267-269, :401-403): the
+    torch generator is seeded from the split key's two words, so different
+    keys give different initial networks (not flax's draws)."""
+    k = as_key(rng_key)
+    return int(k[0]) | (int(k[1]) << 32)
+
+
 def _train(model, loss_fn, rng_key, max_steps: int, lr: float):
     """Adam with element-wise gradient clipping to [-1, 1], stopped after
     max_steps or when the squared norm of the clipped gradients reaches the
@@ -141,7 +150,7 @@ def compute_wasserstein_contraction(sample_Px: Callable, rng_key, X, sample_batc
     X = _as_dev(X)
     dists, mask = _pair_mask(X)
     rng_key, _ = split(rng_key)
-    model = LipschitzNN(X.shape[1]).to(X.device)
+    model = LipschitzNN(X.shape[1], seed=_init_seed(rng_key)).to(X.device)
 
     def Pf_mean(key, n_batches):
         keys = split(key, n_batches)
@@ -168,7 +177,7 @@ def compute_kernel_distance(sample_Px: Callable, sample_Qx: Callable, rng_key, X
     X = _as_dev(X)
     dists, mask = _pair_mask(X)
     rng_key, _ = split(rng_key)
-    model = LipschitzNN(X.shape[1]).to(X.device)
+    model = LipschitzNN(X.shape[1], seed=_init_seed(rng_key)).to(X.device)
     if init_params is not None:
         model.load_state_dict(init_params)
 
@@ -201,7 +210,7 @@ def compute_kernel_distance_1d(sample_Px: Callable, sample_Qx: Callable, rng_key
     xt = _as_dev(x).reshape(-1)
     X = xt.reshape(-1, 1)
     rng_key, _ = split(rng_key)
-    model = LipschitzNN(1).to(X.device)
+    model = LipschitzNN(1, seed=_init_seed(rng_key)).to(X.device)
     if init_params is not None:
         model.load_state_dict(init_params)
 

@@ -72,6 +72,32 @@ AMH_HD amh_u32x4 amh_philox4x32_10(uint32_t c0, uint32_t c1, uint32_t c2, uint32
   return o;
 }
 
+/* The same function with the rounds unrolled (device code only): for
+ * batched draws where several independent streams should interleave (the
+ * pooled noise-ahead blocks).  Not used by default: unrolled rounds raise the
+ * register count of the step kernels. */
+#if defined(__HIPCC__)
+__device__ __forceinline__ amh_u32x4 amh_philox4x32_10_unrolled(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3,
+                                                                uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)AMH_PHILOX_M0 * (uint64_t)c0;
+    const uint64_t p1 = (uint64_t)AMH_PHILOX_M1 * (uint64_t)c2;
+    const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    c0 = hi1 ^ c1 ^ k0;
+    c1 = lo1;
+    c2 = hi0 ^ c3 ^ k1;
+    c3 = lo0;
+    k0 += AMH_PHILOX_W0;
+    k1 += AMH_PHILOX_W1;
+  }
+  amh_u32x4 o;
+  o.v[0] = c0; o.v[1] = c1; o.v[2] = c2; o.v[3] = c3;
+  return o;
+}
+#endif
+
 /* Stream tags (counter word 3).  A chain key plus (tag, counter words) never
  * collides between uses. */
 #define AMH_TAG_CHAINKEY 0x4B48434Du /* derive per-chain key from the run key */
@@ -119,7 +145,7 @@ AMH_HD float amh_logf(float x) {
   r = fmaf(fe, 0.693359375f, r);
   r = (x == INFINITY) ? x : r;
   r = (x == 0.0f) ? -INFINITY : r;
-  r = (x < 0.0f || amh_isnan(x)) ? amh_u2f(0x7FC00000u) : r;
+  r = ((x < 0.0f) | amh_isnan(x)) ? amh_u2f(0x7FC00000u) : r;
   return r;
 }
 

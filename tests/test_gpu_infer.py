@@ -39,7 +39,14 @@ def test_eight_schools_posterior(gpu):
     assert float(s["tau"].std()) == pytest.approx(3.21, abs=0.1)
     assert float(s["theta_base"][:, 0].mean()) == pytest.approx(0.32, abs=0.03)
     assert float(s["theta_base"][:, 0].std()) == pytest.approx(0.99, abs=0.04)
-    assert float(pe.min()) == pytest.approx(40.975, abs=0.5)
+    # the notebook's min U (40.975) is the minimum over ONE chain's 10^4 kept
+    # draws: compare it with the distribution of the per-chain minima over the
+    # same number of draws (each of the C chains here), not with the minimum
+    # over all C x 10^4 draws
+    pmin = np.sort(m.get_extra_fields(group_by_chain=True)["potential_energy"].cpu().numpy().min(axis=1))
+    lo, hi = pmin[int(0.01 * C)], pmin[int(0.99 * C) - 1]
+    print(f"per-chain min U over 1e4 draws: median {np.median(pmin):.3f}, 1%-99% [{lo:.3f}, {hi:.3f}]")
+    assert lo <= 40.975 <= hi
     txt = m.summary_str()
     rows = [ln for ln in txt.split("\n") if ln.strip()]
     assert len(rows) == 1 + 1 + 1 + 8  # header, mu, tau, theta_base[0..7]; theta excluded

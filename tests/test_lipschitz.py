@@ -86,12 +86,14 @@ def test_kernel_distance_1d_notebook_cell101(gpu):
     """asumptions_check.ipynb cell 101: rho(P, Q) between the frozen 1-D
     N(0, 1) kernels with scale 1 and 0.1, n = 1, x = linspace(-5, 5, 100) and
     the notebook's rho_conf (1000 training steps, 1000 x 1000-sample
-    evaluation batches, ratio_rad 5); the notebook prints 0.544187 (its
-    training had not converged: last gradient norm 0.44).  The estimate is a
-    trained lower bound (Adam on a spectrally normalised MLP initialised by a
-    different RNG than flax's) plus the upward bias of a max over 99 noisy
-    adjacent-pair ratios (about 0.02 noise each at 1e6 samples per point), so
-    one run is compared within 0.15 (this build measured 0.457 on MI355X)."""
+    evaluation batches, ratio_rad 5); the notebook prints 0.544187 from one
+    key (its training had not converged: last gradient norm 0.44).  The
+    estimate is a trained lower bound whose value depends on the network's
+    initialisation (flax's draws there, torch's here -- seeded from the key,
+    lipschitz.py:401-403), so one run is one draw of a seed distribution.
+    Measured here over four keys: the residual between their mean and the
+    notebook's number is reported and bounded, and the
+    notebook's value must lie within the spread of the keys' values."""
     import posteriors as P
     from kernels_amd import ARWMH, PRNGKey
     g = P.gaussian(np.zeros(1), cov=np.eye(1))
@@ -102,7 +104,14 @@ def test_kernel_distance_1d_notebook_cell101(gpu):
     fp = lambda key, x, n_samples: k.sample_Pnx(key, x, s_p, 1, n_samples)
     fq = lambda key, x, n_samples: k.sample_Pnx(key, x, s_q, 1, n_samples)
     x = torch.linspace(-5, 5, 100)
-    rho, _, _ = Lz.compute_kernel_distance_1d(fp, fq, PRNGKey(0), x, sample_batch_size=1000, n_train_batches=1,
-                                              n_eval_batches=1000, max_steps=1000, lr=0.1, ratio_rad=5)
-    print("rho", rho)
-    assert abs(rho - 0.544187) < 0.15
+    rhos = []
+    for seed in range(4):
+        rho, _, _ = Lz.compute_kernel_distance_1d(fp, fq, PRNGKey(seed), x, sample_batch_size=1000,
+                                                  n_train_batches=1, n_eval_batches=1000, max_steps=1000, lr=0.1,
+                                                  ratio_rad=5)
+        rhos.append(rho)
+    m, sd = float(np.mean(rhos)), float(np.std(rhos, ddof=1))
+    print(f"cell 101 rho over keys 0..3: {np.round(rhos, 4).tolist()} mean {m:.4f} sd {sd:.4f} "
+          f"residual vs notebook {m - 0.544187:+.4f}")
+    assert abs(m - 0.544187) < 0.15
+    assert min(rhos) - 2 * sd <= 0.544187 <= max(rhos) + 2 * sd
