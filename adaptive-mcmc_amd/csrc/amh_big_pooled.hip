@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
           Xi[cc * kFS + fperm(lane)] = amh_normal_from_bits(o.v[0]);
           if (lane == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
         }
-        if constexpr (N % 4 == 3) __builtin_amdgcn_sched_barrier(0);  // four chains interleaved at most
+        __builtin_amdgcn_sched_barrier(0);  // one chain at a time (the rare path: keeps registers for the rest)
       });
     }
     const bool more = t + 1 < nmine;
@@ -1321,29 +1321,33 @@ __device__ __forceinline__ void ieee_sqrt_div(float x0, float n, float& sq, floa
 }
 
 __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams p) {
-  constexpr int d = 64, P = d * (d + 1) / 2, kQ = d / 4;
+  constexpr int d = 64, P = d * (d + 1) / 2;
   constexpr int S = d + 1;  // LDS row stride of the factor
+  constexpr int kQ8 = d / 8;  // columns per wave in the load / write-out phases
   __shared__ float A[d * S];
-  __shared__ __attribute__((aligned(16))) float cb[2][64];
+  __shared__ __attribute__((aligned(16))) float cols[64][64];  // finished factor columns (broadcast)
   __shared__ float colsum[64];
-  __shared__ int okv;
-  // wave 0's write-out operands, parked here while it factors (they would
-  // otherwise stay live across the factorisation and spill)
-  __shared__ double park_s[kQ][64], park_c[kQ][64];
-  __shared__ float park_l[kQ][64];
+  __shared__ int okv, done;
+  // the factoring waves' write-out operands, parked here while they factor
+  // (they would otherwise stay live across the factorisation)
+  __shared__ double park_s[kQ8][256], park_c[kQ8][256];
+  __shared__ float park_l[kQ8][256];
   const int nred = p.red_blocks;        // > 0: reduce the chunk partials first
   const int base = nred > 0 ? nred : 1;  // blocks [0, base): reduce / update; the rest draw noise
-  if ((int)blockIdx.x >= base) {
-    // extra blocks (one 8-wave block per other CU) beside the single-workgroup
-    // update: the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
-    // Philox(0, i', 0)[1] of every chain, i' = i + K, each chain's row with
-    // its record (the stats kernel uses a row only if the record is its draw)
+  // the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
+  // Philox(0, i', 0)[1] of every chain, i' = i + K, each chain's row with its
+  // record (the stats kernel uses a row only if the record is its draw), by
+  // `nworkers` 8-wave workers: the noise blocks, and the reduce blocks that
+  // do not run the update (after their slice) -- every CU but the update's
+  const int nnoise = (int)gridDim.x - base;  // noise blocks ([base, gridDim.x))
+  const int64_t nworkers = nnoise > 0 ? (int64_t)nnoise + (nred > 0 ? nred - 1 : 0) : 0;
+  auto draw_noise = [&](int64_t worker) {
     const int32_t inext = p.in.i[0] + p.K;
     const int lane = lane_id();
     // wave wv takes the chains wv, wv + nw, ..; the keys of 32 of them arrive
     // in one vector load (lane l: word l & 1 of the (l >> 1)-th)
-    const int64_t wv = (int64_t)(blockIdx.x - base) * 8 + threadIdx.x / 64;
-    const int64_t nw = (int64_t)(gridDim.x - base) * 8;
+    const int64_t wv = worker * 8 + threadIdx.x / 64;
+    const int64_t nw = nworkers * 8;
     // Four chains per group, straight-line (unrolled rounds, no branch:
     // a chain past noise_C repeats the last one and does not store), so the
     // four independent Philox / erfinv chains interleave -- one chain at a
@@ -1374,6 +1378,9 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
         __builtin_amdgcn_sched_barrier(0);
       });
     }
+  };
+  if ((int)blockIdx.x >= base) {
+    draw_noise((int64_t)blockIdx.x - base);
     return;
   }
   const bool coh = nred > 0;  // the sums were just written by other blocks (maybe other XCDs)
@@ -1386,15 +1393,18 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     // pooled_big_post_kernel)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    __shared__ int last;
+    __shared__ int tk;
     int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
-    if (threadIdx.x == 0) last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nred - 1;
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (!last) return;
+    if (tk != nred - 1) {  // not the last: a noise worker
+      if (nnoise > 0) draw_noise((int64_t)nnoise + tk);
+      return;
+    }
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
   }
-  if (threadIdx.x >= 256) return;  // four waves, the CU to themselves
-  if (threadIdx.x < 64) __builtin_amdgcn_s_setprio(3);  // the factorisation wave first on its SIMD
+  // eight waves: wave w loads / forms / writes out the columns w + 8 Q;
+  // waves 0..3 factor (wave f owns the columns 16 f .. 16 f + 15)
   const int tid = threadIdx.x;
   US_INIT
   const int lane = lane_id();
@@ -1403,11 +1413,15 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   auto ldsum = [&](int64_t i) -> double {
     return coh ? __hip_atomic_load(&sums[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sums[i];
   };
+  if (tid == 0) {
+    done = 0;
+    okv = 1;
+  }
   // (0) one batch of loads (issued before anything waits on the scalars)
-  double sig[kQ], cvo[kQ], sv[kQ];
-  float lvo[kQ];
-  static_for<kQ>([&](auto Q) {
-    const int k = w + 4 * Q;
+  double sig[kQ8], cvo[kQ8], sv[kQ8];
+  float lvo[kQ8];
+  static_for<kQ8>([&](auto Q) {
+    const int k = w + 8 * Q;
     const int64_t o = col_off(d, k) + (lane < d - k ? lane : 0);
     cvo[Q] = p.in.cov[o];
     sv[Q] = ldsum(d + o);
@@ -1428,87 +1442,117 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // Sigma' in double, rounded into LDS rows
   {
     const double g = (double)gamma;
-    static_for<kQ>([&](auto Q) {
-      const int k = w + 4 * Q;
+    static_for<kQ8>([&](auto Q) {
+      const int k = w + 8 * Q;
       const double a = (1.0 - g) * cvo[Q];
       const double b = g * (sv[Q] / N);
       sig[Q] = a + b;
       if (lane < d - k) A[(k + lane) * S + k] = (float)sig[Q];
     });
   }
-  if (w == 0) {
-    static_for<kQ>([&](auto Q) {
-      park_s[Q][lane] = sig[Q];
-      park_c[Q][lane] = cvo[Q];
-      park_l[Q][lane] = lvo[Q];
+  if (w < 4) {  // the factoring waves park their write-out operands
+    static_for<kQ8>([&](auto Q) {
+      park_s[Q][tid] = sig[Q];
+      park_c[Q][tid] = cvo[Q];
+      park_l[Q][tid] = lvo[Q];
     });
   }
   US(0)
   __syncthreads();
   US(1)
-  // (1) the factorisation on wave 0 (entries above the diagonal are never
-  // read as operands of valid ones: lanes r < k compute values that are unused)
-  if (w == 0) {
+  // (1) the factorisation, column block f = w on waves 0..3, lane = row.
+  // Every element receives column k's update for k = 0, 1, .. in order (the
+  // oracle's fmaf chain), whichever wave applies it: wave f first applies
+  // the finished columns 0 .. 16 f - 1 of the earlier waves as they appear
+  // in `cols` (LDS, all 64 kept; `done` counts the finished ones), then
+  // factors its own 16 columns.  Column k: pivot (v_readlane), the IEEE
+  // sqrtf / division chain with column k-1's updates of the block's later
+  // columns in its stalls, column k's update of column k + 1 through
+  // v_readlane (the next pivot ready), column k to `cols`.  Entries above
+  // the diagonal are never operands of valid ones.
+  if (w < 4) {
+    const int f = w;
+    const int c0 = 16 * f;
     int ln = lane;  // opaque: keeps the per-column lane tests from being hoisted
     asm volatile("" : "+v"(ln));
-    float a[d];
-    static_for<d>([&](auto K) { a[K] = A[ln * S + K]; });
+    float a[16];
+    static_for<16>([&](auto J) { a[J] = A[ln * S + c0 + J]; });
+    // the earlier waves' columns, in order
+    for (int k = 0; k < c0;) {
+      int avail = __hip_atomic_load(&done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      if (avail <= k) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      if (avail > c0) avail = c0;
+      for (; k < avail; ++k) {
+        const float lr = cols[k][ln];
+        f32x4 pv[4];
+        static_for<4>([&](auto Q) { pv[Q] = *(const f32x4*)&cols[k][c0 + 4 * Q]; });
+        static_for<8>([&](auto J2) {
+          constexpr int j = 2 * J2;
+          const f32x2v r = __builtin_elementwise_fma(f32x2v{-lr, -lr}, f32x2v{pv[j / 4][j % 4], pv[j / 4][j % 4 + 1]},
+                                                     f32x2v{a[j], a[j + 1]});
+          a[j] = r[0];
+          a[j + 1] = r[1];
+        });
+      }
+    }
     bool ok = true;
-    f32x4 pv[16];  // column k-1's broadcast (rows 4Q .. 4Q+3)
+    f32x4 pv[4];  // column k-1's entries of this block's rows c0 .. c0 + 15
     float am1 = 0.0f;
-    static_for<d>([&](auto K) {
-      constexpr int k = K;
-      const float piv = rdlane(a[k], k);
+    static_for<16>([&](auto J) {
+      constexpr int j = J;
+      const int k = c0 + j;
+      const float piv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[j]), k));
       ok = ok && (piv > 0.0f) && amh_isfinite(piv);
-      // ljj = sqrtf(piv), q = a[k] / ljj as the 16 dependent steps of their
-      // IEEE expansions, each followed by four of column k-1's updates of the
-      // columns m >= k+1 (independent of this chain): the in-order wave
-      // issues those in the chain's latency gaps instead of after it
       float ljj, q;
-      ieee_sqrt_div(piv, a[k], ljj, q, [&](auto S) {
-        if constexpr (k >= 1) {
-          // packed: two columns (m, m + 1), m even, per v_pk_fma_f32 (an
-          // IEEE fma per element, the same bits as two fmaf); column k + 1
-          // alone when it is odd
-          constexpr int m0 = ((k + 1) % 2 == 0) ? k + 1 : k + 2;
-          if constexpr (S == 0 && m0 != k + 1) a[k + 1] = fmaf(-am1, pv[(k + 1) / 4][(k + 1) % 4], a[k + 1]);
-          static_for<2>([&](auto J) {
-            constexpr int m = m0 + 2 * (2 * S + J);
-            if constexpr (m + 1 < d) {
-              const f32x2v r = __builtin_elementwise_fma(f32x2v{-am1, -am1}, f32x2v{pv[m / 4][m % 4], pv[m / 4][m % 4 + 1]},
-                                                         f32x2v{a[m], a[m + 1]});
-              a[m] = r[0];
-              a[m + 1] = r[1];
-            }
-          });
+      ieee_sqrt_div(piv, a[j], ljj, q, [&](auto Sl) {
+        // column k-1's updates of this block's columns m >= k + 1 (packed
+        // pairs (m, m + 1), m - c0 even; column k + 1 alone when odd)
+        if constexpr (j >= 1) {
+          constexpr int m0 = ((j + 1) % 2 == 0) ? j + 1 : j + 2;
+          if constexpr (Sl == 0 && m0 != j + 1) a[j + 1] = fmaf(-am1, pv[(j + 1) / 4][(j + 1) % 4], a[j + 1]);
+          constexpr int m = m0 + 2 * Sl;
+          if constexpr (m + 1 < 16) {
+            const f32x2v r = __builtin_elementwise_fma(f32x2v{-am1, -am1}, f32x2v{pv[m / 4][m % 4], pv[m / 4][m % 4 + 1]},
+                                                       f32x2v{a[m], a[m + 1]});
+            a[m] = r[0];
+            a[m + 1] = r[1];
+          }
         }
       });
-      a[k] = (ln == k) ? ljj : q;
-      if constexpr (k + 1 < d) {
-        float* cbk = cb[k & 1];
-        cbk[ln] = a[k];
-        static_for<16>([&](auto Q) {
-          if constexpr (4 * Q + 3 >= k + 2) pv[(int)Q] = *(const f32x4*)&cbk[4 * Q];
+      a[j] = (ln == k) ? ljj : q;
+      cols[k][ln] = a[j];
+      if constexpr (j + 1 < 16) {
+        static_for<4>([&](auto Q) {
+          if constexpr (4 * Q + 3 >= j + 2) pv[(int)Q] = *(const f32x4*)&cols[k][c0 + 4 * Q];
         });
-        am1 = a[k];
-        const float l1 = rdlane(a[k], k + 1);
-        a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
+        am1 = a[j];
+        const float l1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[j]), k + 1));
+        a[j + 1] = fmaf(-a[j], l1, a[j + 1]);
       }
+      // column k is out.  A wave's LDS operations are performed in issue
+      // order, so the column's writes above land before this flag; the empty
+      // asm keeps the compiler from moving them past it (a release store
+      // would also wait here for the pv reads just issued)
+      asm volatile("" ::: "memory");
+      if (ln == 0) __hip_atomic_store(&done, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       __builtin_amdgcn_sched_barrier(0);
     });
-    static_for<d>([&](auto K) {
-      if ((int)K <= ln) A[ln * S + K] = a[K];
+    static_for<16>([&](auto J) {
+      if (c0 + (int)J <= ln) A[ln * S + c0 + J] = a[J];
     });
-    if (lane == 0) okv = ok ? 1 : 0;
+    if (!ok && ln == 0) okv = 0;
   }
   US(2)
   __syncthreads();
   asm volatile("" ::: "memory");  // the parked values are reloaded, not kept in registers
-  if (w == 0) {
-    static_for<kQ>([&](auto Q) {
-      sig[Q] = park_s[Q][lane];
-      cvo[Q] = park_c[Q][lane];
-      lvo[Q] = park_l[Q][lane];
+  if (w < 4) {
+    static_for<kQ8>([&](auto Q) {
+      sig[Q] = park_s[Q][tid];
+      cvo[Q] = park_c[Q][tid];
+      lvo[Q] = park_l[Q][tid];
     });
   }
   US(3)
@@ -1516,9 +1560,9 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // 64-lane butterfly, then the columns (pooled_big_post_kernel's order)
   const bool ok = okv != 0;
   const float e0 = amh_expf(lam), e1 = amh_expf(lamn);
-  float sq[kQ];
-  static_for<kQ>([&](auto Q) {
-    const int k = w + 4 * Q;
+  float sq[kQ8];
+  static_for<kQ8>([&](auto Q) {
+    const int k = w + 8 * Q;
     const int64_t co = col_off(d, k);
     sq[Q] = 0.0f;
     const float lf = A[((k + lane) < d ? k + lane : d - 1) * S + k];
@@ -1532,9 +1576,9 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       p.out.scale[o] = lnw;
     }
   });
-  static_for<kQ>([&](auto Q) {  // independent butterflies, interleaved
+  static_for<kQ8>([&](auto Q) {  // independent butterflies, interleaved
     const float s0 = Grp<64>::sum(sq[Q]);
-    if (lane == 0) colsum[w + 4 * Q] = (s0 + 0.0f) + (0.0f + 0.0f);
+    if (lane == 0) colsum[w + 8 * Q] = (s0 + 0.0f) + (0.0f + 0.0f);
   });
   __syncthreads();
   if (w == 0) {
