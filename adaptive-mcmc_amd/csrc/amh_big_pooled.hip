@@ -905,6 +905,64 @@ __device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, i
   });
 }
 
+// sqrtf(x) and then n / sqrtf(x), spelled out as the compiler's IEEE
+// expansions for gfx950 with f32 denormals on (v_sqrt_f32 + the +-1 ulp
+// residual correction, 2^32 pre-scaling below 2^-96, the zero/+inf class
+// select; v_div_scale / v_rcp / Newton fmas / v_div_fmas / v_div_fixup) --
+// the same instructions in the same order, so the same bits as `sqrtf` and
+// `/` (the oracle's operations).  fill(S), S = 0..15, runs after step S with a
+// scheduling barrier on both sides: independent work placed in the chain's
+// dependency stalls (an in-order wave cannot reorder it there by itself, and
+// the compiler's scheduler does not).
+template <class F>
+__device__ __forceinline__ void ieee_sqrt_div(float x0, float n, float& sq, float& qt, F&& fill) {
+  using I = std::integral_constant<int, 0>;
+  auto step = [&](auto S) {
+    __builtin_amdgcn_sched_barrier(0);
+    fill(S);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  const bool sc = x0 < 0x1p-96f;
+  const float x = sc ? x0 * 0x1p32f : x0;
+  step(std::integral_constant<int, 0>{});
+  float r = __builtin_amdgcn_sqrtf(x);
+  step(std::integral_constant<int, 1>{});
+  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
+  step(std::integral_constant<int, 2>{});
+  const float vp = fmaf(-rm, r, x);
+  step(std::integral_constant<int, 3>{});
+  const float vs = fmaf(-rp, r, x);
+  step(std::integral_constant<int, 4>{});
+  r = (vp <= 0.0f) ? rm : r;
+  r = (vs > 0.0f) ? rp : r;
+  step(std::integral_constant<int, 5>{});
+  r = sc ? r * 0x1p-16f : r;
+  const float s = __builtin_amdgcn_classf(x, 0x260) ? x : r;  // +-0, +inf
+  sq = s;
+  step(std::integral_constant<int, 6>{});
+  bool flag = false, unused = false;
+  const float den = __builtin_amdgcn_div_scalef(n, s, false, &unused);
+  const float num = __builtin_amdgcn_div_scalef(n, s, true, &flag);
+  step(std::integral_constant<int, 7>{});
+  const float rc = __builtin_amdgcn_rcpf(den);
+  step(std::integral_constant<int, 8>{});
+  const float f0 = fmaf(-den, rc, 1.0f);
+  step(std::integral_constant<int, 9>{});
+  const float f1 = fmaf(f0, rc, rc);
+  step(std::integral_constant<int, 10>{});
+  const float mu = num * f1;
+  step(std::integral_constant<int, 11>{});
+  const float f2 = fmaf(-den, mu, num);
+  step(std::integral_constant<int, 12>{});
+  const float f3 = fmaf(f2, f1, mu);
+  step(std::integral_constant<int, 13>{});
+  const float f4 = fmaf(-den, f3, num);
+  step(std::integral_constant<int, 14>{});
+  qt = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(f4, f1, f3, flag), s, n);
+  step(std::integral_constant<int, 15>{});
+  (void)sizeof(I);
+}
+
 template <int NT>
 __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(PooledUpdateParams p) {
   extern __shared__ __attribute__((aligned(16))) float A[];  // A4 layout, float32
@@ -1028,29 +1086,31 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
         // (m >= k+1, read while column k was being formed) are applied; then
         // column k goes to LDS and its next-column update a[k+1] is done with
         // v_readlane.  Every element still sees its updates in column order.
-#ifdef AMH_STAMPS_TWICE
-#pragma unroll 1
-        for (int rep_ = 0; rep_ < 2; ++rep_) {  // diagnostic: second pass with a warm instruction cache
-        if (rep_ == 1) US(5)
-#endif
         f32x4 pv[8];  // column k-1's broadcast values (rows 4q .. 4q+3)
         float am1 = 0.0f;
-#ifndef AMH_UPD_NOCOLS
         static_for<32>([&](auto K) {
           constexpr int k = K;
           const float piv = rdlane(a[k], k);
           ok = ok && (piv > 0.0f) && amh_isfinite(piv);
-          const float ljj = sqrtf(piv);
-          const float q = a[k] / ljj;
-          __builtin_amdgcn_sched_barrier(0);
-          if constexpr (k >= 1) {  // column k-1's updates of rows m >= k+1
-            static_for<8>([&](auto Q) {
-              static_for<4>([&](auto E) {
-                constexpr int m = 4 * Q + E;
-                if constexpr (m >= k + 1) a[m] = fmaf(-am1, pv[(int)Q][(int)E], a[m]);
-              });
-            });
-          }
+          // ljj = sqrtf(piv), q = a[k] / ljj as their IEEE expansions, with
+          // column k-1's updates of the panel's columns m >= k+1 (packed
+          // pairs (m, m + 1), m even; column k + 1 alone when odd) in the
+          // chain's stalls (ieee_sqrt_div; the same bits)
+          float ljj, q;
+          ieee_sqrt_div(piv, a[k], ljj, q, [&](auto Sl) {
+            if constexpr (k >= 1) {
+              constexpr int m0 = ((k + 1) % 2 == 0) ? k + 1 : k + 2;
+              if constexpr (Sl == 0 && m0 != k + 1) a[k + 1] = fmaf(-am1, pv[(k + 1) / 4][(k + 1) % 4], a[k + 1]);
+              constexpr int m = m0 + 2 * Sl;
+              if constexpr (m + 1 < 32) {
+                const f32x2v rr = __builtin_elementwise_fma(f32x2v{-am1, -am1},
+                                                            f32x2v{pv[m / 4][m % 4], pv[m / 4][m % 4 + 1]},
+                                                            f32x2v{a[m], a[m + 1]});
+                a[m] = rr[0];
+                a[m + 1] = rr[1];
+              }
+            }
+          });
           a[k] = (ln == k) ? ljj : q;
           if constexpr (k + 1 < 32) {
             float* cbk = cb + 64 * (k & 1);
@@ -1064,10 +1124,6 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
           }
           __builtin_amdgcn_sched_barrier(0);
         });
-#endif
-#ifdef AMH_STAMPS_TWICE
-        }
-#endif
         US(1)
         if (w == 0 && lane == 0 && !ok) okv = 0;
         // branch-free write-back: lanes with nothing to write (above the
@@ -1262,64 +1318,6 @@ __global__ __launch_bounds__(512) void pooled_reduce64_kernel(const float* __res
   reduce64_slice(partials, n_chunks, V, sums, accumulate, (int)blockIdx.x, false);
 }
 
-// sqrtf(x) and then n / sqrtf(x), spelled out as the compiler's IEEE
-// expansions for gfx950 with f32 denormals on (v_sqrt_f32 + the +-1 ulp
-// residual correction, 2^32 pre-scaling below 2^-96, the zero/+inf class
-// select; v_div_scale / v_rcp / Newton fmas / v_div_fmas / v_div_fixup) --
-// the same instructions in the same order, so the same bits as `sqrtf` and
-// `/` (the oracle's operations).  fill(S), S = 0..15, runs after step S with a
-// scheduling barrier on both sides: independent work placed in the chain's
-// dependency stalls (an in-order wave cannot reorder it there by itself, and
-// the compiler's scheduler does not).
-template <class F>
-__device__ __forceinline__ void ieee_sqrt_div(float x0, float n, float& sq, float& qt, F&& fill) {
-  using I = std::integral_constant<int, 0>;
-  auto step = [&](auto S) {
-    __builtin_amdgcn_sched_barrier(0);
-    fill(S);
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  const bool sc = x0 < 0x1p-96f;
-  const float x = sc ? x0 * 0x1p32f : x0;
-  step(std::integral_constant<int, 0>{});
-  float r = __builtin_amdgcn_sqrtf(x);
-  step(std::integral_constant<int, 1>{});
-  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
-  step(std::integral_constant<int, 2>{});
-  const float vp = fmaf(-rm, r, x);
-  step(std::integral_constant<int, 3>{});
-  const float vs = fmaf(-rp, r, x);
-  step(std::integral_constant<int, 4>{});
-  r = (vp <= 0.0f) ? rm : r;
-  r = (vs > 0.0f) ? rp : r;
-  step(std::integral_constant<int, 5>{});
-  r = sc ? r * 0x1p-16f : r;
-  const float s = __builtin_amdgcn_classf(x, 0x260) ? x : r;  // +-0, +inf
-  sq = s;
-  step(std::integral_constant<int, 6>{});
-  bool flag = false, unused = false;
-  const float den = __builtin_amdgcn_div_scalef(n, s, false, &unused);
-  const float num = __builtin_amdgcn_div_scalef(n, s, true, &flag);
-  step(std::integral_constant<int, 7>{});
-  const float rc = __builtin_amdgcn_rcpf(den);
-  step(std::integral_constant<int, 8>{});
-  const float f0 = fmaf(-den, rc, 1.0f);
-  step(std::integral_constant<int, 9>{});
-  const float f1 = fmaf(f0, rc, rc);
-  step(std::integral_constant<int, 10>{});
-  const float mu = num * f1;
-  step(std::integral_constant<int, 11>{});
-  const float f2 = fmaf(-den, mu, num);
-  step(std::integral_constant<int, 12>{});
-  const float f3 = fmaf(f2, f1, mu);
-  step(std::integral_constant<int, 13>{});
-  const float f4 = fmaf(-den, f3, num);
-  step(std::integral_constant<int, 14>{});
-  qt = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(f4, f1, f3, flag), s, n);
-  step(std::integral_constant<int, 15>{});
-  (void)sizeof(I);
-}
-
 __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams p) {
   constexpr int d = 64, P = d * (d + 1) / 2;
   constexpr int S = d + 1;  // LDS row stride of the factor
@@ -1358,15 +1356,22 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       const uint32_t kv = p.keys[2 * kc + (lane & 1)];
       static_for<8>([&](auto G) {
         if (c32 + nw * (4 * G) >= p.noise_C) return;  // (wave-uniform) no chain of this group left
-        float xv[4];
+        float xv[4], uv[4], wv0[4];
         uint32_t kk0[4], kk1[4], ub[4];
-        static_for<4>([&](auto E) {
+        static_for<4>([&](auto E) {  // amh_normal_from_bits, the tail only where a lane needs it
           constexpr int J = 4 * G + E;
           kk0[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J);
           kk1[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J + 1);
           const amh_u32x4 o = amh_philox4x32_10_unrolled((uint32_t)lane, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0[E], kk1[E]);
-          xv[E] = amh_normal_from_bits(o.v[0]);
+          xv[E] = amh_normal_head(o.v[0], &uv[E], &wv0[E]);
           ub[E] = (uint32_t)__builtin_amdgcn_readlane((int)o.v[1], 0);
+        });
+        static_for<4>([&](auto E) {
+          if (__builtin_amdgcn_ballot_w64(!(wv0[E] < 5.0f)) != 0) {
+            const float pl = amh_erfinv_tail(wv0[E]);
+            xv[E] = (wv0[E] < 5.0f) ? xv[E] : pl;
+          }
+          xv[E] = 1.41421356f * (xv[E] * uv[E]);
         });
         static_for<4>([&](auto E) {
           const int64_t ch = c32 + nw * (4 * G + E);

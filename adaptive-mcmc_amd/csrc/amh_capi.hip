@@ -542,6 +542,16 @@ static bool reduce_fusion_off() {
   return off;
 }
 
+// AMH_POOLED_NOISE_AHEAD=0: the update launch draws no noise for the next
+// step (each stats kernel then draws its own; A/B switch, same bits)
+static bool noise_ahead_off() {
+  static const bool off = [] {
+    const char* e = getenv("AMH_POOLED_NOISE_AHEAD");
+    return e != nullptr && e[0] == '0';
+  }();
+  return off;
+}
+
 // d = 64 with prep_for_update: the last step's chunk partials are left
 // unreduced; *deferred describes them for the update launch, which reduces
 // them first (one launch fewer per pooled block)
@@ -715,7 +725,8 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipMemsetAsync");
     }
     p.scratch = h->upd_buf;
-    if (h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys) {
+    if (h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys &&
+        !noise_ahead_off()) {
       p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows
       p.keys = (const uint32_t*)in->rng_key;
       p.xrec = (uint4*)h->noise_buf;

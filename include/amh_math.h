@@ -226,6 +226,48 @@ AMH_HD float amh_normal_from_bits(uint32_t b) {
   return 1.41421356f * amh_erfinvf(u);
 }
 
+#if defined(__HIPCC__)
+/* amh_normal_from_bits split for batched draws on the device (the same
+ * value): the head gives u, w and the central polynomial; the tail
+ * polynomial of erfinv (w >= 5, |u| > 0.9966: ~0.3% of draws, so about one
+ * wave in five has a lane there) and its sqrtf are needed only when some
+ * lane of the wave has w >= 5, which the caller tests wave-uniformly; the
+ * normal is then 1.41421356 * ((w < 5 ? ps : pl) * u). */
+__device__ __forceinline__ float amh_normal_head(uint32_t b, float* u_out, float* w_out) {
+  const float lo = -0.99999994f;
+  const float f = amh_unif01_from_bits(b);
+  float u = (f * 2.0f) + lo;
+  u = (u < lo) ? lo : u;
+  const float w0 = -amh_logf((1.0f - u) * (1.0f + u));
+  const float ws = w0 - 2.5f;
+  float ps = 2.81022636e-08f;
+  ps = fmaf(ps, ws, 3.43273939e-07f);
+  ps = fmaf(ps, ws, -3.5233877e-06f);
+  ps = fmaf(ps, ws, -4.39150654e-06f);
+  ps = fmaf(ps, ws, 0.00021858087f);
+  ps = fmaf(ps, ws, -0.00125372503f);
+  ps = fmaf(ps, ws, -0.00417768164f);
+  ps = fmaf(ps, ws, 0.246640727f);
+  ps = fmaf(ps, ws, 1.50140941f);
+  *u_out = u;
+  *w_out = w0;
+  return ps;
+}
+__device__ __forceinline__ float amh_erfinv_tail(float w0) {
+  const float wl = sqrtf(w0) - 3.0f;
+  float pl = -0.000200214257f;
+  pl = fmaf(pl, wl, 0.000100950558f);
+  pl = fmaf(pl, wl, 0.00134934322f);
+  pl = fmaf(pl, wl, -0.00367342844f);
+  pl = fmaf(pl, wl, 0.00573950773f);
+  pl = fmaf(pl, wl, -0.0076224613f);
+  pl = fmaf(pl, wl, 0.00943887047f);
+  pl = fmaf(pl, wl, 1.00167406f);
+  pl = fmaf(pl, wl, 2.83297682f);
+  return pl;
+}
+#endif
+
 /* ----------------------------------------------------------- sin/cos ---- */
 /* Cephes-style single precision sin and cos of one argument (the slice
  * angle of ASSS, asss.py:69, :95: |theta| < 2 pi).  theta = k pi/2 + r with
