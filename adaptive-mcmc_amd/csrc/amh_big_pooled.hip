@@ -1337,25 +1337,30 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // record (the stats kernel uses a row only if the record is its draw), by
   // `nworkers` 8-wave workers: the noise blocks, and the reduce blocks that
   // do not run the update (after their slice) -- every CU but the update's
+  // The reduce blocks join ~5 us late (their slice, the write-through and
+  // the ticket first), so they take the chains [split, C) at 70 % of a noise
+  // block's share per wave; the noise blocks take [0, split).
   const int nnoise = (int)gridDim.x - base;  // noise blocks ([base, gridDim.x))
-  const int64_t nworkers = nnoise > 0 ? (int64_t)nnoise + (nred > 0 ? nred - 1 : 0) : 0;
-  auto draw_noise = [&](int64_t worker) {
+  const int nlate = (nnoise > 0 && nred > 0) ? nred - 1 : 0;
+  const int64_t split =
+      nlate > 0 ? (int64_t)((double)p.noise_C * (double)nnoise / ((double)nnoise + 0.7 * (double)nlate)) : p.noise_C;
+  auto draw_noise = [&](int64_t worker, int64_t nworkers, int64_t cbeg, int64_t cend) {
     const int32_t inext = p.in.i[0] + p.K;
     const int lane = lane_id();
-    // wave wv takes the chains wv, wv + nw, ..; the keys of 32 of them arrive
-    // in one vector load (lane l: word l & 1 of the (l >> 1)-th)
-    const int64_t wv = worker * 8 + threadIdx.x / 64;
+    // wave wv takes the chains cbeg + wv, + nw, ..; the keys of 32 of them
+    // arrive in one vector load (lane l: word l & 1 of the (l >> 1)-th)
+    const int64_t wv = cbeg + worker * 8 + threadIdx.x / 64;
     const int64_t nw = nworkers * 8;
     // Four chains per group, straight-line (unrolled rounds, no branch:
     // a chain past noise_C repeats the last one and does not store), so the
     // four independent Philox / erfinv chains interleave -- one chain at a
     // time left the wave waiting on each dependent 64-bit multiply.
-    for (int64_t c32 = wv; c32 < p.noise_C; c32 += 32 * nw) {
+    for (int64_t c32 = wv; c32 < cend; c32 += 32 * nw) {
       int64_t kc = c32 + nw * (lane >> 1);
-      if (kc >= p.noise_C) kc = p.noise_C - 1;
+      if (kc >= cend) kc = cend - 1;
       const uint32_t kv = p.keys[2 * kc + (lane & 1)];
       static_for<8>([&](auto G) {
-        if (c32 + nw * (4 * G) >= p.noise_C) return;  // (wave-uniform) no chain of this group left
+        if (c32 + nw * (4 * G) >= cend) return;  // (wave-uniform) no chain of this group left
         float xv[4], uv[4], wv0[4];
         uint32_t kk0[4], kk1[4], ub[4];
         static_for<4>([&](auto E) {  // amh_normal_from_bits, the tail only where a lane needs it
@@ -1375,7 +1380,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
         });
         static_for<4>([&](auto E) {
           const int64_t ch = c32 + nw * (4 * G + E);
-          if (ch < p.noise_C) {
+          if (ch < cend) {
             p.xi[ch * d + lane] = xv[E];
             if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0[E], kk1[E], ub[E]);
           }
@@ -1384,12 +1389,13 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       });
     }
   };
-  if ((int)blockIdx.x >= base) {
-    draw_noise((int64_t)blockIdx.x - base);
-    return;
-  }
+  // one call site of draw_noise (two inlined copies cost the update path
+  // its registers): noise blocks go straight there, the reduce blocks that
+  // lose the ticket after their slice
+  int64_t nz_worker = (int64_t)blockIdx.x - base, nz_count = nnoise, nz_beg = 0, nz_end = split;
+  bool noise_role = (int)blockIdx.x >= base;
   const bool coh = nred > 0;  // the sums were just written by other blocks (maybe other XCDs)
-  if (nred > 0) {
+  if (!noise_role && nred > 0) {
     reduce64_slice(p.red_partials, p.red_chunks, pooled_big_tile_V_dev(d), p.sums_out, p.red_accumulate,
                    (int)blockIdx.x, true);
     // the last block to finish its slice runs the update: write-through
@@ -1403,10 +1409,19 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tk != nred - 1) {  // not the last: a noise worker
-      if (nnoise > 0) draw_noise((int64_t)nnoise + tk);
-      return;
+      if (nlate == 0) return;
+      noise_role = true;
+      nz_worker = tk;
+      nz_count = nlate;
+      nz_beg = split;
+      nz_end = p.noise_C;
+    } else if (threadIdx.x == 0) {
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     }
-    if (threadIdx.x == 0) __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+  }
+  if (noise_role) {
+    draw_noise(nz_worker, nz_count, nz_beg, nz_end);
+    return;
   }
   // eight waves: wave w loads / forms / writes out the columns w + 8 Q;
   // waves 0..3 factor (wave f owns the columns 16 f .. 16 f + 15)
