@@ -1245,32 +1245,38 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
 // the panel kernel it replaces and of orc_pooled_update_big).  The write-out
 // and as_change (column sums by the 64-lane butterfly, then the columns)
 // follow on all four waves.
-// ------------------------------------------------ d = 64 chunk reduction --
-// The fused d = 64 kernel's float32 partial rows (tile layout, V floats per
+// ------------------------------------------------ chunk reduction, d >= 64 --
+// The fused stats kernels' float32 partial rows (tile layout, V floats per
 // 128-chain chunk) -> the packed double sums, in the bit spec's order
 // (pooled_group4_kernel + pooled_final_kernel): per entry, the chunks of each
 // group of 16 summed in chunk order from 0.0, then the group sums in group
 // order from 0.0 (then += the sums so far when accumulating over a pooled
-// block).  One 512-thread block owns 16 float4 columns of the row for every
+// block; with `fp`, the update's Sigma' entry as pooled_final_kernel forms
+// it).  One 512-thread block owns 16 float4 columns of the row for every
 // group: thread (tg, c) sums group 32 gt + tg of column c into LDS, then 64
-// threads (column, component) add the 32 group sums in order, tile by tile.
+// threads (column, component) add the group sums in order, tile by tile.
 // One launch instead of two; with `coherent` the sums go out write-through
 // (agent-scope stores) for a reader in another XCD.
-constexpr int kRedCols = 16;  // float4 columns per reduce block
+constexpr int kRedCols = 16;  // float4 columns per reduce block (32 groups per pass)
 constexpr int kRedGrp = 16;   // chunks per group (pooled_reduce's kRedGroup)
 int pooled_reduce64_blocks(int64_t V) { return (int)((V / 4 + kRedCols - 1) / kRedCols); }
 
-__device__ __forceinline__ void reduce64_slice(const float* __restrict__ partials, int64_t n_chunks, int64_t V,
-                                               double* sums, int accumulate, int blk, bool coherent) {
-  __shared__ double gs[32][kRedCols][4];
+// NCOL float4 columns x (512 / NCOL) groups per pass: 16 x 32, or 32 x 16
+// when there are at most 16 groups (d = 256 at C = 32,768), so no thread idles
+template <int NCOL = kRedCols>
+__device__ __forceinline__ void reduce_tiles_slice(const float* __restrict__ partials, int64_t n_chunks, int64_t V,
+                                                   double* sums, int accumulate, int blk, int tile_d,
+                                                   const FinalPrep& fp, bool coherent) {
+  constexpr int GT = 512 / NCOL;  // groups per pass
+  __shared__ double gs[GT][NCOL][4];
   const int tid = threadIdx.x;
-  const int c = tid & (kRedCols - 1), tg = tid >> 4;  // 512 threads: 16 columns x 32 groups
-  const int64_t v4 = (int64_t)blk * kRedCols + c;
+  const int c = tid % NCOL, tg = tid / NCOL;
+  const int64_t v4 = (int64_t)blk * NCOL + c;
   const bool col_ok = 4 * v4 < V;
   const int64_t n_groups = (n_chunks + kRedGrp - 1) / kRedGrp;
-  const int fc = tid >> 2, comp = tid & 3;  // finishing threads (tid < 64)
+  const int fc = tid >> 2, comp = tid & 3;  // finishing threads (tid < 4 NCOL)
   double tot = 0.0;
-  for (int64_t g0 = 0; g0 < n_groups; g0 += 32) {
+  for (int64_t g0 = 0; g0 < n_groups; g0 += GT) {
     const int64_t g = g0 + tg;
     double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
     if (g < n_groups && col_ok) {
@@ -1293,29 +1299,36 @@ __device__ __forceinline__ void reduce64_slice(const float* __restrict__ partial
     gs[tg][c][2] = s2;
     gs[tg][c][3] = s3;
     __syncthreads();
-    if (tid < 64) {
-      const int64_t ng = n_groups - g0 < 32 ? n_groups - g0 : 32;
+    if (tid < 4 * NCOL) {
+      const int64_t ng = n_groups - g0 < GT ? n_groups - g0 : GT;
       for (int q = 0; q < ng; ++q) tot += gs[q][fc][comp];  // group order
     }
     __syncthreads();
   }
-  if (tid < 64) {
-    const int64_t u = 4 * ((int64_t)blk * kRedCols + fc) + comp;
-    const int64_t v = u < V ? tile_to_packed(u, V, kF) : -1;
-    if (v >= 0) {
-      const double sv = accumulate ? sums[v] + tot : tot;
-      if (coherent) {
-        __hip_atomic_store(&sums[v], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        sums[v] = sv;
-      }
-    }
+  if (tid < 4 * NCOL) {
+    const int64_t u = 4 * ((int64_t)blk * NCOL + fc) + comp;
+    if (u < V) final_entry(u, tot, V, sums, accumulate, tile_d, fp, coherent);
   }
 }
 
-__global__ __launch_bounds__(512) void pooled_reduce64_kernel(const float* __restrict__ partials, int64_t n_chunks,
-                                                              int64_t V, double* sums, int accumulate) {
-  reduce64_slice(partials, n_chunks, V, sums, accumulate, (int)blockIdx.x, false);
+template <int NCOL>
+__global__ __launch_bounds__(512) void pooled_reduce_tiles_kernel(const float* __restrict__ partials, int64_t n_chunks,
+                                                                  int64_t V, double* sums, int accumulate, int tile_d,
+                                                                  FinalPrep fp) {
+  reduce_tiles_slice<NCOL>(partials, n_chunks, V, sums, accumulate, (int)blockIdx.x, tile_d, fp, false);
+}
+
+hipError_t launch_reduce_tiles(const float* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
+                               int tile_d, const FinalPrep& fp, hipStream_t s) {
+  const int64_t n_groups = (n_chunks + kRedGrp - 1) / kRedGrp;
+  if (n_groups <= 16) {
+    hipLaunchKernelGGL(pooled_reduce_tiles_kernel<32>, dim3((unsigned)((V / 4 + 31) / 32)), dim3(512), 0, s, partials,
+                       n_chunks, V, sums, accumulate, tile_d, fp);
+  } else {
+    hipLaunchKernelGGL(pooled_reduce_tiles_kernel<16>, dim3((unsigned)((V / 4 + 15) / 16)), dim3(512), 0, s, partials,
+                       n_chunks, V, sums, accumulate, tile_d, fp);
+  }
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams p) {
@@ -1396,8 +1409,8 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   bool noise_role = (int)blockIdx.x >= base;
   const bool coh = nred > 0;  // the sums were just written by other blocks (maybe other XCDs)
   if (!noise_role && nred > 0) {
-    reduce64_slice(p.red_partials, p.red_chunks, pooled_big_tile_V_dev(d), p.sums_out, p.red_accumulate,
-                   (int)blockIdx.x, true);
+    reduce_tiles_slice(p.red_partials, p.red_chunks, pooled_big_tile_V_dev(d), p.sums_out, p.red_accumulate,
+                       (int)blockIdx.x, d, FinalPrep{}, true);
     // the last block to finish its slice runs the update: write-through
     // stores done (vmcnt(0)), then an agent-scope ticket; the last arriver
     // reads the sums with agent-scope loads (the cross-XCD hand-off of
@@ -1704,11 +1717,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
 }
 
 // --------------------------------------------------------------- launchers --
-hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
-                         hipStream_t s, int tile_d = 0, FinalPrep fp = FinalPrep{});
-
-// chains per chunk of the sums (bit spec): 64 at d = 64 (the fused kernel's
-// block), 256 above
+// chains per chunk of the sums (bit spec): 128 at every d >= 64
 int64_t pooled_big_chunks(int64_t C, int d) {
   const int64_t ch = (d == kF) ? kFChunk : kFB;
   return (C + ch - 1) / ch;
@@ -1728,10 +1737,8 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     if (e != hipSuccess) return e;
     (void)V;
     if (p.defer_reduce) return hipSuccess;  // the update launch reduces (run_pooled_big_update)
-    const int64_t Vt = pooled_big_tile_V(d);
-    hipLaunchKernelGGL(pooled_reduce64_kernel, dim3((unsigned)pooled_reduce64_blocks(Vt)), dim3(512), 0, s,
-                       (const float*)p.partials, nch, Vt, sums, p.accumulate);
-    return hipGetLastError();
+    return launch_reduce_tiles((const float*)p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, d, FinalPrep{},
+                               s);
   }
   {
     const int nt = d / 32;
@@ -1759,7 +1766,8 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     e = hipGetLastError();
     if (e != hipSuccess) return e;
     (void)pep;
-    return pooled_reduce(p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, s, d, p.prep);
+    // one launch (was pooled_group4_kernel + pooled_final_kernel)
+    return launch_reduce_tiles((const float*)p.partials, nch, pooled_big_tile_V(d), sums, p.accumulate, d, p.prep, s);
   }
 }
 

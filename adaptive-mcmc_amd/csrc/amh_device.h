@@ -748,4 +748,38 @@ __device__ inline int64_t tile_to_packed(int64_t u, int64_t Vt, int d, int* prow
 }
 
 
+// the update's 4-row-aligned layout (amh_big_pooled.hip a4_base)
+__device__ __forceinline__ int fp_a4_base(int d, int j) {
+  const int q = j >> 2;
+  return 4 * (q * d - 2 * q * (q - 1)) + (j & 3) * (d - 4 * q) - (j & ~3);
+}
+
+// entry u of the sums once its total over the groups is known: the packed
+// index (tile layout above d = 64), accumulation over the steps of a pooled
+// block, and (one rank, amh_pooled_step_k) the update's Sigma' entry
+__device__ __forceinline__ void final_entry(int64_t u, double tot, int64_t V, double* sums, int accumulate,
+                                            int tile_d, const FinalPrep& fp, bool coherent = false) {
+  int row = -1, col = -1;
+  const int64_t v = tile_d ? tile_to_packed(u, V, tile_d, &row, &col) : u;
+  if (v < 0) return;
+  const double sv = accumulate ? sums[v] + tot : tot;
+  if (coherent) {  // read by another block, maybe in another XCD: write-through
+    __hip_atomic_store(&sums[v], sv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    sums[v] = sv;
+  }
+  if (fp.scratch != nullptr && col >= 0) {
+    // Sigma' = (1-g) Sigma + g S_dd / N in float, as pooled_big_prep_kernel
+    const int d = tile_d;
+    const int32_t it = fp.i[0];
+    const double gm = (double)amh_lr_gamma(pooled_block_n(it, fp.W, fp.K), fp.a);
+    const int64_t o = v - d;
+    const double a = (1.0 - gm) * fp.cov[o];
+    const double b = gm * (sv / fp.N);
+    fp.scratch[fp_a4_base(d, col) + row] = (float)(a + b);
+    if (u == d) ((int*)fp.scratch)[d * (d + 4) / 2 + 4] = it + fp.K;  // the next step's i (noise blocks)
+  }
+}
+
+
 }  // namespace amh

@@ -244,64 +244,6 @@ __global__ __launch_bounds__(256) void pooled_group_kernel(const T* __restrict__
   gsum[g * V + v] = s;
 }
 
-// the large-d stats kernel's float32 partials (their widening to double is
-// exact, so storing them as float halves the traffic and changes no bit),
-// four consecutive entries per thread (V % 4 == 0: the tile row is padded)
-__global__ __launch_bounds__(256) void pooled_group4_kernel(const float* __restrict__ partials, int64_t n_chunks,
-                                                            int64_t V, double* __restrict__ gsum) {
-  const int64_t v4 = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t g = blockIdx.y;
-  if (4 * v4 >= V) return;
-  const int64_t c1 = (g + 1) * kRedGroup < n_chunks ? (g + 1) * kRedGroup : n_chunks;
-  float4 x[kRedGroup];
-#pragma unroll
-  for (int q = 0; q < kRedGroup; ++q)
-    x[q] = (g * kRedGroup + q < c1) ? ((const float4*)(partials + (g * kRedGroup + q) * V))[v4] : float4{};
-  double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;  // chunk order
-#pragma unroll
-  for (int q = 0; q < kRedGroup; ++q)
-    if (g * kRedGroup + q < c1) {
-      s0 += (double)x[q].x;
-      s1 += (double)x[q].y;
-      s2 += (double)x[q].z;
-      s3 += (double)x[q].w;
-    }
-  double* o = gsum + g * V + 4 * v4;
-  o[0] = s0;
-  o[1] = s1;
-  o[2] = s2;
-  o[3] = s3;
-}
-
-// the update's 4-row-aligned layout (amh_big_pooled.hip a4_base)
-__device__ __forceinline__ int fp_a4_base(int d, int j) {
-  const int q = j >> 2;
-  return 4 * (q * d - 2 * q * (q - 1)) + (j & 3) * (d - 4 * q) - (j & ~3);
-}
-
-// entry u of the sums once its total over the groups is known: the packed
-// index (tile layout above d = 64), accumulation over the steps of a pooled
-// block, and (one rank, amh_pooled_step_k) the update's Sigma' entry
-__device__ __forceinline__ void final_entry(int64_t u, double tot, int64_t V, double* sums, int accumulate,
-                                            int tile_d, const FinalPrep& fp) {
-  int row = -1, col = -1;
-  const int64_t v = tile_d ? tile_to_packed(u, V, tile_d, &row, &col) : u;
-  if (v < 0) return;
-  const double sv = accumulate ? sums[v] + tot : tot;
-  sums[v] = sv;
-  if (fp.scratch != nullptr && col >= 0) {
-    // Sigma' = (1-g) Sigma + g S_dd / N in float, as pooled_big_prep_kernel
-    const int d = tile_d;
-    const int32_t it = fp.i[0];
-    const double gm = (double)amh_lr_gamma(pooled_block_n(it, fp.W, fp.K), fp.a);
-    const int64_t o = v - d;
-    const double a = (1.0 - gm) * fp.cov[o];
-    const double b = gm * (sv / fp.N);
-    fp.scratch[fp_a4_base(d, col) + row] = (float)(a + b);
-    if (u == d) ((int*)fp.scratch)[d * (d + 4) / 2 + 4] = it + fp.K;  // the next step's i (noise blocks)
-  }
-}
-
 __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restrict__ gsum, int64_t n_groups, int64_t V,
                                                            double* sums, int accumulate, int tile_d, FinalPrep fp) {
   const int64_t u = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -329,17 +271,16 @@ __global__ __launch_bounds__(256) void pooled_final_kernel(const double* __restr
 
 int64_t pooled_scratch_rows(int64_t n_chunks) { return n_chunks + (n_chunks + kRedGroup - 1) / kRedGroup; }
 
+// d < 64: double partial rows, two launches (group sums, then the groups);
+// d >= 64 reduces its float32 tile rows in one launch
+// (amh_big_pooled.hip, pooled_reduce_tiles_kernel)
 hipError_t pooled_reduce(const double* partials, int64_t n_chunks, int64_t V, double* sums, int accumulate,
                          hipStream_t s, int tile_d = 0, FinalPrep fp = FinalPrep{}) {
   const int64_t n_groups = (n_chunks + kRedGroup - 1) / kRedGroup;
   double* gsum = const_cast<double*>(partials) + n_chunks * V;
   const unsigned vb = (unsigned)((V + 255) / 256);
-  if (tile_d)  // the large-d stats kernel's float32 partials, V % 4 == 0
-    hipLaunchKernelGGL(pooled_group4_kernel, dim3((unsigned)((V / 4 + 255) / 256), (unsigned)n_groups), dim3(256), 0,
-                       s, (const float*)partials, n_chunks, V, gsum);
-  else
-    hipLaunchKernelGGL(pooled_group_kernel<double>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials,
-                       n_chunks, V, gsum);
+  hipLaunchKernelGGL(pooled_group_kernel<double>, dim3(vb, (unsigned)n_groups), dim3(256), 0, s, partials,
+                     n_chunks, V, gsum);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(pooled_final_kernel, dim3(vb), dim3(256), 0, s, (const double*)gsum, n_groups, V, sums,
