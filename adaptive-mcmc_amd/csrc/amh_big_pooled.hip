@@ -127,30 +127,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   const int32_t it = p.i[0] + p.i_add;  // step i_add of a pooled block
   const float el = amh_expf(p.lam[0]);
   const float mu_l = p.mu[lane];  // lane = coordinate k in the chain-major phases
-  // A operands in registers: lane (i, h) of MFMA m holds row 32 T + i, column 2 m + h
   float aL[32];
-  {
-    // unconditional loads in one batch (above the diagonal: the row's
-    // diagonal entry, replaced by 0 once loaded); P rows to LDS in fperm order
-    const int r = 32 * T + i;
-    float pv[16];
-    static_for<32>([&](auto M) {
-      const int k = 2 * M + h;
-      aL[M] = p.L[pk(d, r, k <= r ? k : r)];
-    });
-    static_for<16>([&](auto N) { pv[N] = p.model.data[d + ((tid >> 6) + 4 * (int)N) * d + (tid & 63)]; });
-    static_for<32>([&](auto M) {
-      if (2 * M + h > r) aL[M] = 0.0f;
-    });
-    static_for<16>([&](auto N) {
-      const int row = (tid >> 6) + 4 * N, k = tid & 63;
-      lds[f64::PP + row * kFS + fperm(k)] = pv[N];
-    });
-    if (tid < d) {
-      lds[f64::MP + fperm(tid)] = p.model.data[tid];
-      lds[f64::MN + tid] = p.model.data[tid];
-    }
-  }
   // the block's sub-chunks, flat: t -> chunk blockIdx.x + gridDim.x (t / kSub),
   // sub-chunk t % kSub; only the grid's last chunk can be ragged, so the valid
   // ones are a prefix
@@ -194,11 +171,36 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   f32x16 sacc = f32x16{};  // S_dd of the chunk so far (waves 0..2)
   float sd = 0.0f, sa = 0.0f;  // S_d (wave 3, lane = coordinate), S_a (wave 3 lane 0)
   int cnt = 0;
+  // the first sub-chunk's loads go out before the shared operands' (one
+  // memory latency in the prologue instead of two)
   if (nmine > 0) {
     load_sub(0);
     load_pe(0);
-    store_z();
   }
+  // A operands in registers: lane (i, h) of MFMA m holds row 32 T + i, column 2 m + h
+  {
+    // unconditional loads in one batch (above the diagonal: the row's
+    // diagonal entry, replaced by 0 once loaded); P rows to LDS in fperm order
+    const int r = 32 * T + i;
+    float pv[16];
+    static_for<32>([&](auto M) {
+      const int k = 2 * M + h;
+      aL[M] = p.L[pk(d, r, k <= r ? k : r)];
+    });
+    static_for<16>([&](auto N) { pv[N] = p.model.data[d + ((tid >> 6) + 4 * (int)N) * d + (tid & 63)]; });
+    static_for<32>([&](auto M) {
+      if (2 * M + h > r) aL[M] = 0.0f;
+    });
+    static_for<16>([&](auto N) {
+      const int row = (tid >> 6) + 4 * N, k = tid & 63;
+      lds[f64::PP + row * kFS + fperm(k)] = pv[N];
+    });
+    if (tid < d) {
+      lds[f64::MP + fperm(tid)] = p.model.data[tid];
+      lds[f64::MN + tid] = p.model.data[tid];
+    }
+  }
+  if (nmine > 0) store_z();
   lds_barrier();
   FS(14)
   for (int64_t t = 0; t < nmine; ++t) {
