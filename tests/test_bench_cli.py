@@ -27,3 +27,11 @@ def test_self_spawn_starts_n_ranks():
     # (the parent stops the other rank once one has failed, so it may not get to print)
     assert 1 <= (r.stderr + r.stdout).count("no GPU visible") <= 2
     assert "WORLD_SIZE" not in (r.stderr + r.stdout)  # the children got the launcher environment
+
+
+def test_configs_names_checked_before_any_gpu_call():
+    r = _run(["--configs", "diamonds,bogus"], {})
+    assert r.returncode != 0
+    assert "unknown ['bogus']" in (r.stderr + r.stdout)
+    r = _run(["--configs", "diamonds", "--gpus", "2"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode != 0
