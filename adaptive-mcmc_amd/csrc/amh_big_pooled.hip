@@ -1512,10 +1512,19 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     asm volatile("" : "+v"(ln));
     float a[16];
     static_for<16>([&](auto J) { a[J] = A[ln * S + c0 + J]; });
-    // the earlier waves' columns, in order
+    // the earlier waves' columns, in order (the wait is bounded: a wave
+    // that never sees its column marks the update failed -- the factor is
+    // then kept -- rather than hang the GPU; producers never wait, so this
+    // does not happen)
+    bool stuck = false;
+    int spins = 0;
     for (int k = 0; k < c0;) {
       int avail = __hip_atomic_load(&done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (avail <= k) {
+        if (++spins > (1 << 22)) {
+          stuck = true;
+          break;
+        }
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
@@ -1578,7 +1587,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     static_for<16>([&](auto J) {
       if (c0 + (int)J <= ln) A[ln * S + c0 + J] = a[J];
     });
-    if (!ok && ln == 0) okv = 0;
+    if ((!ok || stuck) && ln == 0) okv = 0;
   }
   US(2)
   __syncthreads();
