@@ -91,6 +91,13 @@ int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d
       if (n_data != 2 * (4 + 2 * Kc + Kc * Kc)) { *why = "diamonds_suffstat data must hold 2 (4 + 2 Kc + Kc^2) floats"; return -1; }
       return (int)(Kc + 2);
     }
+    case AMH_MODEL_MIXTURE: {
+      if (nip < 1) { *why = "mixture needs iparams {K}"; return -1; }
+      if (ip[0] < 1 || ip[0] > 8) { *why = "mixture needs 1 <= K <= 8 components"; return -1; }
+      if (n_data != 3 * ip[0]) { *why = "mixture data must hold 3*K floats"; return -1; }
+      if (d < 1 || d > 16) { *why = "mixture needs 1 <= d <= 16"; return -1; }
+      return d;
+    }
     default:
       *why = "unknown model id";
       return -1;
@@ -185,7 +192,7 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
   h->model_id = 0;  // unbound until the whole binding has succeeded
   h->model.data = data;
   const bool dia = model_id == AMH_MODEL_DIAMONDS || model_id == AMH_MODEL_DIAMONDS_SS;
-  h->model.n = (model_id == AMH_MODEL_KIDIQ || dia) ? iparams[0] : 0;
+  h->model.n = (model_id == AMH_MODEL_KIDIQ || model_id == AMH_MODEL_MIXTURE || dia) ? iparams[0] : 0;
   h->model.k = dia ? iparams[1] : 0;
   h->n_data = n_data;
   if (model_id == AMH_MODEL_DIAMONDS && amh::split_model(model_id, dm)) {

@@ -575,6 +575,54 @@ struct DiamondsSSM {
   }
 };
 
+// Mixture of K <= 8 univariate normals, applied to every coordinate
+// (asumptions_check.ipynb cells 61-62: potential_fn = -MixtureSameFamily(
+// Categorical(w), Normal(m, s)).log_prob(x), summed over coordinates, which
+// at d = 1 -- the notebook's case -- is the scalar it returns).
+// data = [c (K) | m (K) | s (K)] with c_k = log w_k - log(sqrt(2 pi) s_k)
+// (host, float64, then rounded), staged in LDS.  Per coordinate:
+//   lp_k = c_k - 0.5 t_k^2, t_k = (x - m_k) / s_k  (numpyro Normal.log_prob)
+//   v = log(sum_k exp(lp_k - M)) + M, M = max_k lp_k or 0 if not finite
+//   (jax.nn.logsumexp; the sum in k order from 0).
+constexpr int kMixtureKMax = 8;
+template <int G>
+struct MixtureM {
+  struct Ctx {
+    int K;
+  };
+  static __host__ __device__ size_t lds_bytes(const ModelArgs& m, int) { return (size_t)(3 * m.n) * sizeof(float); }
+  static __device__ void stage(float* lds, const ModelArgs& m, int) {
+    for (int64_t k = threadIdx.x; k < 3 * m.n; k += blockDim.x) lds[k] = m.data[k];
+  }
+  static __device__ __forceinline__ Ctx prepare(const ModelArgs& m, int, int) { return Ctx{(int)m.n}; }
+  static __device__ __forceinline__ float potential(float x, int r, int d, const Ctx& c, const float* lds) {
+    const int K = c.K;
+    const uint32_t a0 = lds_addr(lds);
+    const uint32_t nb = (uint32_t)K * 4u;
+    float lp[kMixtureKMax];
+    float mx = -INFINITY;
+    static_for<kMixtureKMax>([&](auto Kc) {
+      constexpr int k = Kc;
+      lp[k] = 0.0f;
+      if (k < K) {
+        float ck = lds_ld1<4 * k>(a0), mk = lds_ld1<4 * k>(a0 + nb), sk = lds_ld1<4 * k>(a0 + 2u * nb);
+        lds_wait(ck, mk, sk);
+        const float t = (x - mk) / sk;
+        lp[k] = ck - 0.5f * (t * t);
+        mx = (lp[k] > mx) ? lp[k] : mx;
+      }
+    });
+    mx = (mx == INFINITY || mx == -INFINITY || mx != mx) ? 0.0f : mx;
+    float S = 0.0f;
+    static_for<kMixtureKMax>([&](auto Kc) {
+      constexpr int k = Kc;
+      if (k < K) S = S + amh_expf(lp[k] - mx);
+    });
+    const float v = (r < d) ? (amh_logf(S) + mx) : 0.0f;
+    return -Grp<G>::sum(v);
+  }
+};
+
 // Potential evaluated outside the step kernel (split path, amh_split.hip):
 // the step kernel reads U(z') from StepParams::ext_pe instead of calling
 // potential(); init leaves pe for the batched potential kernel to fill.
@@ -720,6 +768,13 @@ static hipError_t dispatch(int model_id, int d, F&& f) {
     case AMH_MODEL_DIAMONDS_SS:
       if (d < 3 || d > 32) return hipErrorInvalidValue;
       return f.template operator()<32, DiamondsSSM, false>();
+    case AMH_MODEL_MIXTURE:
+      if (d <= 1) return f.template operator()<1, MixtureM, false>();
+      if (d <= 2) return f.template operator()<2, MixtureM, false>();
+      if (d <= 4) return f.template operator()<4, MixtureM, false>();
+      if (d <= 8) return f.template operator()<8, MixtureM, false>();
+      if (d <= 16) return f.template operator()<16, MixtureM, false>();
+      return hipErrorInvalidValue;
     default:
       return hipErrorInvalidValue;
   }

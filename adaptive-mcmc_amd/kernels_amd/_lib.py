@@ -21,6 +21,7 @@ AMH_MODEL_EIGHT_SCHOOLS = 2
 AMH_MODEL_KIDIQ = 3
 AMH_MODEL_DIAMONDS = 4
 AMH_MODEL_DIAMONDS_SS = 5
+AMH_MODEL_MIXTURE = 6
 AMH_STEP_PROPOSAL_READY = 1
 AMH_STEP_KEEP_PROPOSAL = 2
 

@@ -300,6 +300,15 @@ class ARWMH:
             else:
                 self._chained = (tuple(weakref.ref(t) for t in out), tuple(t._version for t in out))
 
+    def _ensure_bound(self):
+        """sample_Pnx needs no init() with a raw potential_fn (arwmh.py:230-270
+        calls only self._potential_fn and self.sample): bind the device
+        potential on first use.  A model needs its data (init's model_kwargs)."""
+        if self._handle is None:
+            if self._potential_fn is None:
+                raise RuntimeError("call init() (or get_init_adapt_state()) first")
+            self._bind(0, {}, _device_index(self._device))
+
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""
         _lib.require_gpu(z)
@@ -324,8 +333,7 @@ class ARWMH:
     def sample_Pnx(self, rng_key, x, adapt_state, n=1, n_samples=1000, jit_inner=True):
         """arwmh.py:230-270: n frozen-kernel steps from every x[i] for n_samples
         chains each, all sharing one adapt_state; returns [n_points, n_samples, d]."""
-        if self._handle is None:
-            raise RuntimeError("call init() (or get_init_adapt_state()) first")
+        self._ensure_bound()
         dev = torch.device("cuda", _device_index(self._device))
         x = torch.as_tensor(x.cpu() if hasattr(x, "cpu") else np.asarray(x), dtype=torch.float32)
         x = x.reshape(-1, self._dim).to(dev).contiguous()

@@ -145,8 +145,7 @@ class ASSS(ARWMH):
         """asss.py:267-296: n frozen-kernel transitions from every x[i] for
         n_samples chains each, sharing adapt_state = (loc, scale); returns
         [n_points, n_samples, d]."""
-        if self._handle is None:
-            raise RuntimeError("call init() (or get_init_adapt_state()) first")
+        self._ensure_bound()
         dev = torch.device("cuda", _device_index(self._device))
         d = self._dim
 

@@ -9,8 +9,9 @@ Python callable, so each model here is a registry entry that knows
   * how to pack the model's data for the device potential (include/amh.h),
   * how to map unconstrained draws back to constrained sites (postprocess).
 
-Entries: eight_schools (non-centred), kidiq_kidscore_momhsiq, diamonds and a
-dense Gaussian potential (the build's benchmark targets).
+Entries: eight_schools (non-centred), kidiq_kidscore_momhsiq, diamonds, a
+dense Gaussian potential (the build's benchmark targets) and the notebook's
+normal mixture potential (asumptions_check.ipynb cells 61-62).
 """
 from __future__ import annotations
 
@@ -249,6 +250,54 @@ def correlated_gaussian(d: int = 64, log10_kappa: float = 2.0, seed: int = None)
     s = 10.0 ** (-k / 2 + k * np.arange(d) / max(d - 1, 1))
     cov = (Q * s) @ Q.T
     return gaussian(np.zeros(d), cov=cov)
+
+
+# ------------------------------------------------------------------- mixture --
+@dataclass
+class Mixture:
+    """Univariate normal mixture on every coordinate, a raw potential_fn
+    plug-in: U(x) = -sum_r log sum_k w_k N(x_r; m_k, s_k) (asumptions_check.ipynb
+    cells 61-62, `-mixture.log_prob(x)` of numpyro's MixtureSameFamily; the
+    notebook's x is 1-D, so its vector-valued potential has one entry)."""
+    weights: np.ndarray
+    locs: np.ndarray
+    scales: np.ndarray
+    dim: int = 1
+    model_id: int = field(default=_lib.AMH_MODEL_MIXTURE, init=False)
+    name: str = field(default="mixture", init=False)
+
+    def pack(self, device) -> Tuple[torch.Tensor, Tuple[int, ...]]:
+        w = np.asarray(self.weights, np.float64)
+        s = np.asarray(self.scales, np.float64)
+        c = np.log(w) - np.log(np.sqrt(2 * np.pi) * s)
+        arr = np.concatenate([c, np.asarray(self.locs, np.float64), s]).astype(np.float32)
+        return torch.as_tensor(arr, device=device), (len(w),)
+
+    def __call__(self, z):
+        """Host evaluation (float64), for diagnostics only."""
+        x = np.asarray(_np(z), np.float64)[..., None]
+        lp = np.log(np.asarray(self.weights, np.float64)) - 0.5 * ((x - self.locs) / self.scales) ** 2 \
+            - np.log(np.sqrt(2 * np.pi) * np.asarray(self.scales, np.float64))
+        mx = lp.max(axis=-1, keepdims=True)
+        return -(np.log(np.exp(lp - mx).sum(axis=-1)) + mx[..., 0]).sum(axis=-1)
+
+
+def mixture(weights, locs, scales, dim: int = 1) -> Mixture:
+    w = np.asarray(weights, np.float64).reshape(-1)
+    m = np.asarray(locs, np.float64).reshape(-1)
+    s = np.asarray(scales, np.float64).reshape(-1)
+    if not (w.shape == m.shape == s.shape) or not 1 <= w.size <= 8:
+        raise ValueError("mixture needs 1..8 components with matching weights / locs / scales")
+    if np.any(w <= 0) or abs(w.sum() - 1.0) > 1e-6 or np.any(s <= 0):
+        raise ValueError("mixture weights must be positive and sum to 1, scales positive")
+    if not 1 <= int(dim) <= 16:
+        raise ValueError("mixture supports 1 <= dim <= 16")
+    return Mixture(w, m, s, int(dim))
+
+
+# asumptions_check.ipynb cell 61: 1/2 N(-1, 0.1) + 1/2 N(1, 0.1)
+def notebook_mixture() -> Mixture:
+    return mixture([0.5, 0.5], [-1.0, 1.0], [0.1, 0.1])
 
 
 REGISTRY = {

@@ -63,3 +63,44 @@ def collect_states_logscale(rng_key, sampler, model_data: dict, n_pow: int = 6, 
             sampler.sample_(state, thin)
             snaps.append(_snapshot(state))
     return concat_trees(snaps)
+
+
+# ------------------------------------------------ local contraction estimates --
+# asumptions_check.ipynb cells 81-82 (notebook-local helpers the analysis runs
+# through sample_Pnx + wasserstein_1d): tau_x(P^n) = W1(P^n(x_l, .),
+# P^n(x_r, .)) / (x_r - x_l) for a pair of points around every x of a 1-D grid.
+# As in the notebook, every x's pair is drawn with the same rng_key (so the
+# pairs at different x share their per-sample keys).
+def _taus_from_pairs(kernel, rng_key, pairs: np.ndarray, adapt_state, n: int, n_samples: int,
+                     divisor: float = None) -> np.ndarray:
+    from utils_amd.evaluation import wasserstein_1d
+    out = np.empty(pairs.shape[0], np.float64)
+    for i, (xl, xr) in enumerate(pairs):
+        X = np.array([[xl], [xr]], np.float32)
+        P = kernel.sample_Pnx(rng_key, X, adapt_state, n, n_samples)  # [2, n_samples, 1]
+        w = wasserstein_1d(P[0, :, 0], P[1, :, 0])
+        out[i] = float(w) / (divisor if divisor is not None else float(np.float32(xr) - np.float32(xl)))
+    return out
+
+
+def get_taus_n(rng_key, kernel, X, adapt_state, n: int = 1, n_samples: int = 10000, eps: float = 5e-2) -> np.ndarray:
+    """Cell 81 (ARWMH): the pair (x - eps, x + eps), W1 / (2 eps)."""
+    x = np.asarray(X.cpu() if hasattr(X, "cpu") else X, np.float32).reshape(-1)
+    e = np.float32(eps)
+    pairs = np.stack([x - e, x + e], axis=1)
+    return _taus_from_pairs(kernel, rng_key, pairs, adapt_state, n, n_samples, divisor=2 * eps)
+
+
+def get_taus_n_sss(rng_key, kernel, X, adapt_state, n: int = 1, n_samples: int = 10000,
+                   eps: float = 1e-1) -> np.ndarray:
+    """Cell 82 (ASSS): the pair is +-eps in the stereographic angle,
+    phi = 2 arctan((x - loc) / scale), x_lr = tan((phi -+ eps) / 2) scale + loc,
+    divided by x_r - x_l (float32, as the notebook's jnp arithmetic)."""
+    loc = np.float32(np.asarray(adapt_state[0].cpu() if hasattr(adapt_state[0], "cpu") else adapt_state[0]).reshape(-1)[0])
+    sc = np.float32(np.asarray(adapt_state[1].cpu() if hasattr(adapt_state[1], "cpu") else adapt_state[1]).reshape(-1)[0])
+    x = np.asarray(X.cpu() if hasattr(X, "cpu") else X, np.float32).reshape(-1)
+    phi = np.float32(2) * np.arctan((x - loc) / sc)
+    e = np.float32(eps)
+    xl = np.tan((phi - e) / np.float32(2)) * sc + loc
+    xr = np.tan((phi + e) / np.float32(2)) * sc + loc
+    return _taus_from_pairs(kernel, rng_key, np.stack([xl, xr], axis=1).astype(np.float32), adapt_state, n, n_samples)

@@ -58,9 +58,13 @@ enum {
   AMH_MODEL_EIGHT_SCHOOLS = 2, /* data: [y (J) | sigma (J) | log sigma (J)], d = J + 2     */
   AMH_MODEL_KIDIQ = 3,         /* data: [kid (N) | mom_hs (N) | mom_iq (N)], d = 4          */
   AMH_MODEL_DIAMONDS = 4,      /* data: [Xc (N*Kc) | Y (N)], d = Kc + 2, Kc = K - 1        */
-  AMH_MODEL_DIAMONDS_SS = 5    /* diamonds through float64 sufficient statistics, passed as
+  AMH_MODEL_DIAMONDS_SS = 5,   /* diamonds through float64 sufficient statistics, passed as
                                   2 floats each: [N, ybar, A, sT, t (Kc), sx (Kc), Gm (Kc*Kc)],
                                   n_data = 2 (4 + 2 Kc + Kc^2), iparams {N, K}, 3 <= d <= 32 */
+  AMH_MODEL_MIXTURE = 6        /* K-component univariate normal mixture on every coordinate
+                                  (asumptions_check.ipynb cells 61-62): data [c (K) | m (K) |
+                                  s (K)], c_k = log w_k - log(sqrt(2 pi) s_k); iparams {K},
+                                  1 <= K <= 8, n_data = 3 K, 1 <= d <= 16 */
 };
 
 typedef struct amh_config {

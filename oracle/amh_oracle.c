@@ -31,7 +31,7 @@
 
 #define ORC_DMAX 64
 
-enum { ORC_GAUSSIAN = 1, ORC_EIGHT_SCHOOLS = 2, ORC_KIDIQ = 3, ORC_DIAMONDS = 4, ORC_DIAMONDS_SS = 5 };
+enum { ORC_GAUSSIAN = 1, ORC_EIGHT_SCHOOLS = 2, ORC_KIDIQ = 3, ORC_DIAMONDS = 4, ORC_DIAMONDS_SS = 5, ORC_MIXTURE = 6 };
 
 typedef struct {
   int32_t model_id;
@@ -280,6 +280,34 @@ static float pot_diamonds_ss(const orc_cfg* cfg, const float* x, int G) {
   return -(((ll + lpb) + lpi) + lps);
 }
 
+/* K-component univariate normal mixture on every coordinate
+ * (asumptions_check.ipynb cells 61-62; amh_device.h MixtureM).  data =
+ * [c (K) | m (K) | s (K)], c_k = log w_k - log(sqrt(2 pi) s_k); n_data = K.
+ * Per coordinate: lp_k = c_k - 0.5 t^2, t = (x - m_k) / s_k; the
+ * jax.nn.logsumexp over k (max, non-finite max -> 0, sum in k order). */
+static float pot_mixture(const orc_cfg* cfg, const float* x, int G) {
+  const int K = (int)cfg->n_data;
+  const float* c = cfg->data;
+  const float* m = cfg->data + K;
+  const float* s = cfg->data + 2 * K;
+  float v[ORC_DMAX];
+  for (int r = 0; r < G; ++r) {
+    if (r >= cfg->d) { v[r] = 0.0f; continue; }
+    float lp[8];
+    float mx = -INFINITY;
+    for (int k = 0; k < K; ++k) {
+      const float t = (x[r] - m[k]) / s[k];
+      lp[k] = c[k] - 0.5f * (t * t);
+      mx = (lp[k] > mx) ? lp[k] : mx;
+    }
+    mx = (mx == INFINITY || mx == -INFINITY || mx != mx) ? 0.0f : mx;
+    float S = 0.0f;
+    for (int k = 0; k < K; ++k) S = S + amh_expf(lp[k] - mx);
+    v[r] = amh_logf(S) + mx;
+  }
+  return -group_sum(v, G);
+}
+
 static float pot_gaussian_big(const orc_cfg* cfg, const float* x);
 
 float orc_potential1(const orc_cfg* cfg, const float* x) {
@@ -291,6 +319,7 @@ float orc_potential1(const orc_cfg* cfg, const float* x) {
     case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
     case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
     case ORC_DIAMONDS_SS: return pot_diamonds_ss(cfg, x, G);
+    case ORC_MIXTURE: return pot_mixture(cfg, x, G);
     default: return NAN;
   }
 }
@@ -672,6 +701,7 @@ static float orc_potential_g(const orc_cfg* cfg, const float* x, int G) {
     case ORC_KIDIQ: return pot_kidiq(cfg, x, G);
     case ORC_DIAMONDS: return pot_diamonds(cfg, x, G);
     case ORC_DIAMONDS_SS: return pot_diamonds_ss(cfg, x, G);
+    case ORC_MIXTURE: return pot_mixture(cfg, x, G);
     default: return NAN;
   }
 }

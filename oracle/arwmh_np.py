@@ -196,6 +196,17 @@ def diamonds_potential(z, Xc, Y):
     return -lp
 
 
+def mixture_potential(z, weights, locs, scales):
+    """asumptions_check.ipynb cells 61-62: -MixtureSameFamily(Categorical(w),
+    Normal(m, s)).log_prob(x), summed over the coordinates of z (a scalar at
+    d = 1, the notebook's case)."""
+    x = np.atleast_1d(np.asarray(z, np.float64))[:, None]
+    lp = np.log(np.asarray(weights, np.float64)) + normal_lp(x, np.asarray(locs, np.float64),
+                                                            np.asarray(scales, np.float64))
+    mx = lp.max(axis=1, keepdims=True)
+    return -float(np.sum(np.log(np.exp(lp - mx).sum(axis=1)) + mx[:, 0]))
+
+
 def gaussian_potential(z, m, P, c0):
     diff = np.asarray(z) - m
     return 0.5 * diff @ (P @ diff) + c0

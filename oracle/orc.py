@@ -21,7 +21,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # `make -C oracle asan`, run by tests/test_oracle_asan.py)
 _LIB_PATH = os.environ.get("AMH_ORACLE_LIB") or os.path.join(_HERE, "build", "libamh_oracle.so")
 
-GAUSSIAN, EIGHT_SCHOOLS, KIDIQ, DIAMONDS, DIAMONDS_SS = 1, 2, 3, 4, 5
+GAUSSIAN, EIGHT_SCHOOLS, KIDIQ, DIAMONDS, DIAMONDS_SS, MIXTURE = 1, 2, 3, 4, 5, 6
 
 _P = ctypes.c_void_p
 _I64 = ctypes.c_int64

@@ -31,6 +31,10 @@ def make_case(kind: str, d: int = None):
         arr, ip = P.diamonds_suffstat.pack_fn(mk)
         N, K = ip
         return dict(model=P.diamonds_suffstat), mk, orc.Model(orc.DIAMONDS_SS, K + 1, arr, n_data=N, k_data=K)
+    if kind == "mixture":  # asumptions_check.ipynb cell 61, on every coordinate
+        mx = P.notebook_mixture() if (d or 1) == 1 else P.mixture([0.5, 0.5], [-1.0, 1.0], [0.1, 0.1], dim=d)
+        data, ip = mx.pack("cpu")
+        return dict(potential_fn=mx), {}, orc.Model(orc.MIXTURE, mx.dim, data.numpy(), n_data=ip[0])
     raise ValueError(kind)
 
 

@@ -50,7 +50,7 @@ def _step_compare(kind, pre, orc, C=48, d=None):
 
 
 @pytest.mark.parametrize("kind,d", [("gaussian", 12), ("gaussian", 64), ("eight_schools", None), ("kidiq", None),
-                                    ("diamonds", None)])
+                                    ("diamonds", None), ("mixture", 1), ("mixture", 3)])
 @pytest.mark.parametrize("pre", [0, 1, 23])
 def test_oracle_step_matches_literal(kind, d, pre, orc):
     _step_compare(kind, pre, orc, C=24 if kind in ("diamonds", "gaussian") else 48, d=d)

@@ -114,3 +114,34 @@ def test_gaussian_potential_against_scipy():
         got = np.array([lit.gaussian_potential(xx, m, Pm, c0) for xx in x])
         # data are the float32-rounded precision and constant: compare at float32 resolution
         np.testing.assert_allclose(got, want, rtol=1e-5, atol=1e-4)
+
+
+def test_mixture_potential_against_scipy():
+    """asumptions_check.ipynb cell 61: -log(1/2 N(x; -1, .1) + 1/2 N(x; 1, .1)),
+    summed over coordinates; the literal restatement, the host evaluation of
+    posteriors.Mixture and the C oracle against scipy's densities."""
+    import orc
+    import posteriors as P
+    mx = P.notebook_mixture()
+    x = np.linspace(-3.0, 3.0, 601)
+    ref = -np.log(0.5 * stats.norm.pdf(x, -1.0, 0.1) + 0.5 * stats.norm.pdf(x, 1.0, 0.1))
+    lit_u = np.array([lit.mixture_potential(v, [0.5, 0.5], [-1.0, 1.0], [0.1, 0.1]) for v in x])
+    np.testing.assert_allclose(lit_u, ref, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(mx(x[:, None]), ref, rtol=1e-12, atol=1e-12)
+    data, ip = mx.pack("cpu")
+    om = orc.Model(orc.MIXTURE, 1, data.numpy(), n_data=ip[0])
+    u32 = orc.potential(om, x.astype(np.float32)[:, None])
+    np.testing.assert_allclose(u32, ref, rtol=2e-6, atol=2e-5)
+    # far tails: log-sum-exp keeps the potential finite (no underflow to +inf)
+    far = orc.potential(om, np.array([[-30.0], [30.0]], np.float32))
+    np.testing.assert_allclose(far, [-(np.log(0.5) + stats.norm.logpdf(-30.0, -1, .1)),
+                                     -(np.log(0.5) + stats.norm.logpdf(30.0, 1, .1))], rtol=1e-6)
+    # several coordinates and three components
+    m3 = P.mixture([0.2, 0.3, 0.5], [-2.0, 0.0, 1.5], [0.5, 1.0, 0.25], dim=5)
+    d3, ip3 = m3.pack("cpu")
+    om3 = orc.Model(orc.MIXTURE, 5, d3.numpy(), n_data=ip3[0])
+    z = np.random.default_rng(0).normal(size=(200, 5))
+    ref3 = -np.log(sum(w * stats.norm.pdf(z, m, s) for w, m, s in [(0.2, -2, .5), (0.3, 0, 1), (0.5, 1.5, .25)])).sum(1)
+    np.testing.assert_allclose(orc.potential(om3, z.astype(np.float32)), ref3, rtol=3e-6, atol=3e-5)
+    with pytest.raises(ValueError):
+        P.mixture([0.5, 0.6], [0, 1], [1, 1])

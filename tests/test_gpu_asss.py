@@ -49,7 +49,8 @@ def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
 
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 600), ("gaussian", 5, 517), ("gaussian", 16, 300),
                                       ("gaussian", 33, 130), ("eight_schools", None, 400), ("kidiq", None, 257),
-                                      ("diamonds", None, 66), ("diamonds_ss", None, 300)])
+                                      ("diamonds", None, 66), ("diamonds_ss", None, 300), ("mixture", 1, 1000),
+                                      ("mixture", 3, 200)])
 def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
     """ASSS.sample (one launch per step, out of place) vs oracle, 25 steps."""
     k, st, om, ost = _init(kind, C, orc, d=d, num_warmup=8)

@@ -26,7 +26,7 @@ def _init(kind, C, gpu, orc, seed=0, d=None, num_warmup=0):
     return k, st, om, ost
 
 
-@pytest.mark.parametrize("kind", ["gaussian", "eight_schools", "kidiq", "diamonds", "diamonds_ss"])
+@pytest.mark.parametrize("kind", ["gaussian", "eight_schools", "kidiq", "diamonds", "diamonds_ss", "mixture"])
 def test_init_bitexact(kind, gpu, orc):
     k, st, om, ost = _init(kind, 333, gpu, orc)
     assert_state_bitequal(st, ost, f"{kind} init")
@@ -34,7 +34,8 @@ def test_init_bitexact(kind, gpu, orc):
 
 @pytest.mark.parametrize("kind,d", [("gaussian", 64), ("gaussian", 5), ("gaussian", 16), ("gaussian", 33),
                                     ("eight_schools", None), ("kidiq", None), ("diamonds", None), ("diamonds_ss", None),
-                                    ("gaussian", 96), ("gaussian", 256)])
+                                    ("gaussian", 96), ("gaussian", 256), ("mixture", 1), ("mixture", 3),
+                                    ("mixture", 16)])
 def test_potential_bitexact(kind, d, gpu, orc):
     k, st, om, ost = _init(kind, 8, gpu, orc, d=d)
     z = np.random.default_rng(1).normal(size=(1000, om.d)).astype(np.float32)
@@ -45,7 +46,8 @@ def test_potential_bitexact(kind, d, gpu, orc):
 
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("gaussian", 7, 517), ("gaussian", 32, 300),
                                       ("eight_schools", None, 400), ("kidiq", None, 257),
-                                      ("diamonds", None, 66), ("diamonds_ss", None, 333)])
+                                      ("diamonds", None, 66), ("diamonds_ss", None, 333), ("mixture", 1, 1000),
+                                      ("mixture", 5, 300)])
 def test_single_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.sample (one launch per step) vs oracle step(n_steps=1), 40 steps."""
     k, st, om, ost = _init(kind, C, gpu, orc, d=d, num_warmup=10)

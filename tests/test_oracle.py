@@ -40,6 +40,8 @@ def lit_potential(kind, om):
     if kind == "diamonds":
         N, Kc = om.n_data, om.k_data - 1
         return lambda z: lit.diamonds_potential(z, data[:N * Kc].reshape(N, Kc), data[N * Kc:])
+    if kind == "mixture":  # the notebook's weights / locs / scales (helpers.make_case)
+        return lambda z: lit.mixture_potential(z, [0.5, 0.5], [-1.0, 1.0], [0.1, 0.1])
     raise ValueError(kind)
 
 
@@ -88,7 +90,7 @@ def test_nan_potential_rejects():
 # ------------------------------------------------- C oracle vs literal numpy --
 @pytest.mark.parametrize("kind,dim", [("gaussian", 12), ("eight_schools", None), ("kidiq", None),
                                       ("diamonds", None), ("diamonds_ss", None), ("gaussian", 128),
-                                      ("gaussian", 256)])
+                                      ("gaussian", 256), ("mixture", 1), ("mixture", 3)])
 @pytest.mark.parametrize("pre_steps", [0, 1, 37])
 def test_oracle_step_matches_literal(kind, dim, pre_steps, orc):
     """One teacher-forced transition (identical noise) of the C oracle against
