@@ -1359,8 +1359,10 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   const int nlate = (nnoise > 0 && nred > 0) ? nred - 1 : 0;
   const int64_t split =
       nlate > 0 ? (int64_t)((double)p.noise_C * (double)nnoise / ((double)nnoise + 0.7 * (double)nlate)) : p.noise_C;
+  // the noise position, read before any block can reach the update's write of
+  // out.i (in place, in == out): a late reduce worker reads it in a register
+  const int32_t inext = p.in.i[0] + p.K;
   auto draw_noise = [&](int64_t worker, int64_t nworkers, int64_t cbeg, int64_t cend) {
-    const int32_t inext = p.in.i[0] + p.K;
     const int lane = lane_id();
     // wave wv takes the chains cbeg + wv, + nw, ..; the keys of 32 of them
     // arrive in one vector load (lane l: word l & 1 of the (l >> 1)-th)
@@ -1421,7 +1423,9 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     __syncthreads();
     __shared__ int tk;
     int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
-    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // acquire-release at agent scope: this block's sums are released with the
+    // ticket and the last arriver acquires every other block's
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tk != nred - 1) {  // not the last: a noise worker
       if (nlate == 0) return;
@@ -1588,6 +1592,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       if (c0 + (int)J <= ln) A[ln * S + c0 + J] = a[J];
     });
     if ((!ok || stuck) && ln == 0) okv = 0;
+    if (stuck && ln == 0 && p.err_flag != nullptr) *p.err_flag = 1;  // reported by the next call
   }
   US(2)
   __syncthreads();
@@ -1710,7 +1715,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
     const float cs = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
     __hip_atomic_store(&colsum[k], __float_as_uint(cs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == d - 1;
+    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == d - 1;
   }
   __syncthreads();
   if (!last) return;

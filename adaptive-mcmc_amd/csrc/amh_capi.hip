@@ -35,6 +35,8 @@ struct amh_handle {
   int64_t noise_cap = 0;       // chains the noise buffer holds
   int64_t noise_C = 0;         // chains of the last stats call, whose keys are at noise_keys
   const uint32_t* noise_keys = nullptr;
+  int* err_host = nullptr;     // pooled d = 64: host-mapped device error flag (PooledUpdateParams::err_flag)
+  int* err_dev = nullptr;      // ... its device address
   std::string err;
 };
 
@@ -49,6 +51,20 @@ int fail(amh_handle* h, int code, const std::string& msg) {
 
 int hip_fail(amh_handle* h, hipError_t e, const char* where) {
   return fail(h, AMH_EHIP, std::string(where) + ": " + hipGetErrorString(e));
+}
+
+const char* const kUpdateStuck =
+    "amh_pooled_update (d = 64): a factoring wave's bounded wait for an earlier wave's columns ran out in an "
+    "earlier launch; that update kept the factor and covariance (the run no longer follows the bit spec)";
+
+// a device-side failure flagged by an earlier (asynchronous) launch: reported
+// by the handle's next pooled call and by amh_last_error, then cleared
+int check_device_flag(amh_handle* h) {
+  if (h && h->err_host && *(volatile int*)h->err_host != 0) {
+    *(volatile int*)h->err_host = 0;
+    return fail(h, AMH_EHIP, kUpdateStuck);
+  }
+  return AMH_OK;
 }
 
 bool same_buffers(const amh_state& a, const amh_state& b) {
@@ -126,7 +142,10 @@ extern "C" {
 
 int amh_version(void) { return AMH_ABI_VERSION; }
 
-const char* amh_last_error(const amh_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+const char* amh_last_error(const amh_handle* h) {
+  if (h && h->err_host && *(volatile int*)h->err_host != 0) const_cast<amh_handle*>(h)->err = kUpdateStuck;
+  return h ? h->err.c_str() : g_err.c_str();
+}
 
 int amh_create(const amh_config* cfg, int device, amh_handle** out) {
   if (!cfg || !out) return fail(nullptr, AMH_EINVAL, "amh_create: null argument");
@@ -163,6 +182,7 @@ int amh_destroy(amh_handle* h) {
     if (h->upd_buf) (void)hipFree(h->upd_buf);
     if (h->xpack) (void)hipFree(h->xpack);
     if (h->noise_buf) (void)hipFree(h->noise_buf);
+    if (h->err_host) (void)hipHostFree(h->err_host);
   }
   delete h;
   return AMH_OK;
@@ -539,24 +559,32 @@ int amh_pooled_sums_size(int32_t dim, int64_t* v) {
 // prep_for_update: the update follows in the same library call with no
 // exchange in between (amh_pooled_step_k on one rank), so the large-d
 // reduction's last kernel also forms that update's Sigma'
-// AMH_POOLED_FUSED_REDUCE=0: keep the d = 64 reduction in its own launch
-// (A/B switch; the bits are the same either way)
+// A/B switches of the diagnostic build only (-DAMH_DIAG, `make stamps`; the
+// bits are the same either way, the release library reads no environment):
+// AMH_POOLED_FUSED_REDUCE=0 keeps the d = 64 reduction in its own launch;
+// AMH_POOLED_NOISE_AHEAD=0 draws no noise ahead (each stats kernel draws its own)
 static bool reduce_fusion_off() {
+#ifdef AMH_DIAG
   static const bool off = [] {
     const char* e = getenv("AMH_POOLED_FUSED_REDUCE");
     return e != nullptr && e[0] == '0';
   }();
   return off;
+#else
+  return false;
+#endif
 }
 
-// AMH_POOLED_NOISE_AHEAD=0: the update launch draws no noise for the next
-// step (each stats kernel then draws its own; A/B switch, same bits)
 static bool noise_ahead_off() {
+#ifdef AMH_DIAG
   static const bool off = [] {
     const char* e = getenv("AMH_POOLED_NOISE_AHEAD");
     return e != nullptr && e[0] == '0';
   }();
   return off;
+#else
+  return false;
+#endif
 }
 
 // d = 64 with prep_for_update: the last step's chunk partials are left
@@ -577,6 +605,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_pooled_stats: no model bound");
   if (!pooled_ok(in) || !z_out || !pe_out || !sums || num_chains < 1 || k_steps < 1)
     return fail(h, AMH_EINVAL, "amh_pooled_stats: bad arguments");
+  if (int rc = check_device_flag(h)) return rc;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
   const int d = h->cfg.dim;
@@ -711,6 +740,7 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
   if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
     return fail(h, AMH_EINVAL, "amh_pooled_update: k_steps must be >= 1 and divide num_warmup");
+  if (int rc = check_device_flag(h)) return rc;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipSetDevice");
   amh::PooledUpdateParams p{};
@@ -732,6 +762,15 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipMemsetAsync");
     }
     p.scratch = h->upd_buf;
+    if (p.d == 64 && h->err_host == nullptr) {
+      e = hipHostMalloc((void**)&h->err_host, sizeof(int), hipHostMallocMapped);
+      if (e == hipSuccess) {
+        *h->err_host = 0;
+        e = hipHostGetDevicePointer((void**)&h->err_dev, h->err_host, 0);
+      }
+      if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipHostMalloc");
+    }
+    p.err_flag = h->err_dev;
     if (h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys &&
         !noise_ahead_off()) {
       p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows

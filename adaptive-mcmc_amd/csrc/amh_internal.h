@@ -6,6 +6,12 @@
 
 #include "../../include/amh.h"
 
+// the phase-stamp build is a diagnostic build: it also honours the A/B
+// environment switches (amh_kernels.hip, amh_capi.hip)
+#if defined(AMH_STAMPS) && !defined(AMH_DIAG)
+#define AMH_DIAG 1
+#endif
+
 namespace amh {
 
 // Learning-rate table size: gamma_n for n < 2^20 is precomputed on the host
@@ -152,6 +158,10 @@ struct PooledUpdateParams {
   int64_t red_chunks;
   int32_t red_accumulate, red_blocks;
   double* sums_out;
+  // host-mapped flag (the handle's): set when the d = 64 update's bounded
+  // wait on an earlier wave's columns runs out (the factor is then kept);
+  // the next library call on the handle reports it (amh_capi.hip)
+  int* err_flag;
 };
 int pooled_reduce64_blocks(int64_t V);  // reduce blocks of the d = 64 partial rows
 

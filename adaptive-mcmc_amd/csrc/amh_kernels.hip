@@ -1240,17 +1240,25 @@ struct PnxF {
   hipError_t operator()() { return launch_pnx<D, M, E>(p, s); }
 };
 
+// A/B switches (the general kernel for d = 64; the data movement alone) exist
+// only in the diagnostic build (-DAMH_DIAG, `make stamps`): the release
+// library never reads the environment, so no setting can change its work.
 static bool step64_enabled() {
+#ifdef AMH_DIAG
   static const bool on = [] {
     const char* e = getenv("AMH_STEP64");
     return !(e != nullptr && e[0] == '0');
   }();
   return on;
+#else
+  return true;
+#endif
 }
 
 hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
-  // the headline shape: d = 64 Gaussian, LDS-staged write-back (AMH_STEP64=0 selects the general kernel)
+  // the headline shape: d = 64 Gaussian, LDS-staged write-back
   if (model_id == AMH_MODEL_GAUSSIAN && p.d == 64 && p.ext_pe == nullptr && step64_enabled()) {
+#ifdef AMH_DIAG
     static const bool move_only = [] {  // diagnostic: the data movement alone (tools/membound.py)
       const char* e = getenv("AMH_S64_MOVE_ONLY");
       return e != nullptr && e[0] == '1';
@@ -1260,6 +1268,7 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
       q.n_steps = 0;
       return launch_step64<kS64Waves>(q, s);
     }
+#endif
     return launch_step64<kS64Waves>(p, s);
   }
   // diamonds at the reference shape: compile-time d (immediate offsets)

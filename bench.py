@@ -95,7 +95,7 @@ def measured_traffic(C: int, d: int):
 
 def step_kernel_name(d: int) -> str:
     """The kernel the headline leg launches (amh_kernels.hip run_step dispatch)."""
-    if d == 64 and os.environ.get("AMH_STEP64", "1") != "0":
+    if d == 64:
         return "arwmh_step64_kernel<16> (d = 64 specialisation, 16 waves/CU)"
     return f"arwmh_step_kernel<{d}, GaussianM>"
 
@@ -305,7 +305,7 @@ def pooled_line(ctx, r, total, d, C):
             "collective": coll, "clock_warm": r["clock_warm"]}
 
 
-def ess_leg(k, st, burn_in=20000, T=1000):
+def ess_leg(k, st, burn_in=20000, T=1000, headline_s_per_step=None):
     """ESS/s of the headline's own chains (all of them): after the timed region
     they adapt for `burn_in` more steps (fused launches), then T recorded
     transitions in one fused launch that collects z and U on the device; ESS
@@ -330,6 +330,10 @@ def ess_leg(k, st, burn_in=20000, T=1000):
     del x, cz
     vals.append(float(ess_of(cp.t())))
     return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": C, "draws": T, "seconds": el,
+            "ess_per_s_timing": ("ess_min / the wall time of the one FUSED run() launch that recorded the T "
+                                 "draws (state in registers between steps)"),
+            "ess_per_s_at_headline_rate": (min(vals) / (T * headline_s_per_step)
+                                           if headline_s_per_step else None),
             "chains_source": "the headline run's own chains, continued after its timed region",
             "burn_in": burn_in, "steps_before_burn_in": i0, "mean_accept_prob_after_burn_in": acc_burn,
             "mean_accept_prob_window": float(st2.mean_accept_prob.mean()), "coords": coords + ["U"],
@@ -635,6 +639,16 @@ def configs_main(names, steps):
 
 
 # ------------------------------------------------------------------- main --
+def refuse_overrides(environ=os.environ):
+    """The bench measures the release libamh.so as the driver runs it: any
+    AMH_* variable (a library path, or the diagnostic build's A/B switches,
+    which the release library ignores anyway) is refused, not silently
+    measured."""
+    bad = sorted(k for k in environ if k.startswith("AMH_"))
+    if bad:
+        raise SystemExit(f"bench.py: unset {', '.join(bad)} (the bench times the release libamh.so only)")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -650,6 +664,7 @@ def main():
     ap.add_argument("--configs", nargs="?", const=",".join(CONFIG_NAMES), default=None,
                     help="per-config lines instead of the headline (comma list; default all): " + ",".join(CONFIG_NAMES))
     args = ap.parse_args()
+    refuse_overrides()
     if args.configs is not None:
         if args.gpus != 1:
             raise SystemExit("--configs runs on one GPU")
@@ -698,7 +713,8 @@ def main():
                                 ("pooled_overlap", 1, True)):
                 pr = leg_pooled(ctx, g, C, 0, max(args.steps, 32), 16, K=K, overlap=ov, burn_in=256 * K)
                 sub[name] = pooled_line(ctx, pr, C, d, C)
-        ess = ess_leg(r["kernel"], r["state"]) if extra and not args.no_ess else None
+        ess = (ess_leg(r["kernel"], r["state"], headline_s_per_step=r["wall"] / args.steps)
+               if extra and not args.no_ess else None)
         cpu = cpu_baseline(g, d) if extra and not args.no_cpu_baseline else None
         line = {"metric": metric, "value": value, "unit": "chain-steps/s", "n_gpus": 1, "steps": args.steps,
                 "warmup": args.warmup, "ms_per_step": r["wall"] / args.steps * 1e3, "higher_is_better": True,
@@ -720,7 +736,7 @@ def main():
     achieved = flops / (stats_ms * 1e-3) / 1e12
     roofline = {"bound": "mfma", "achieved": achieved, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                 "frac": achieved / FP32_PEAK_TFLOPS, "traffic": None, "kernel_ms": stats_ms,
-                "kernel": ("pooled_fused64_kernel (amh_pooled_stats_k: transitions + 64-chain chunk sums on MFMA)"
+                "kernel": ("pooled_fused64_kernel (amh_pooled_stats_k: transitions + 128-chain chunk sums on MFMA)"
                            if d == 64 else "pooled stats (amh_pooled_stats_k: transitions + chunk sums)"),
                 "algorithmic_flops_per_launch": flops}
     sub = {}
@@ -739,6 +755,12 @@ def main():
         sub["regime_a"] = {"value": total * args.steps / ra["wall"], "unit": "chain-steps/s", "clock_warm": ra["clock_warm"],
                            "ms_per_step": ra["wall"] / args.steps * 1e3, "kernel_ms": ra["kern_ms"],
                            "collective": "none (chains independent, BASELINE configs[1] per GPU)"}
+    cpu = None
+    if rank == 0 and extra and not args.no_cpu_baseline:
+        # the same pooled transition + update on the host (C oracle, bounded
+        # sample of one rank's chains), after every rank has finished timing
+        cpu = cpu_pooled(_orc_model("gaussian", g), C)
+        cpu["sample"] += " (one rank's share of config 5; no all-reduce on the host)"
     if rank == 0:
         line = {"metric": metric, "value": head["value"], "unit": "chain-steps/s", "n_gpus": world,
                 "steps": head["steps"], "warmup": args.warmup, "ms_per_step": head["ms_per_step"],
@@ -747,7 +769,7 @@ def main():
                                         f"({total} in total), all_reduce(sum) of the pooled sums every step "
                                         f"(BASELINE.json configs[4])"),
                            "chains_per_gpu": C, "dim": d, "parallelism": ctx.parallelism(f"chains sharded x{world}")},
-                "roofline": roofline, "cpu_baseline": None, "clock_warm": head["clock_warm"], "pooled": head, **sub}
+                "roofline": roofline, "cpu_baseline": cpu, "clock_warm": head["clock_warm"], "pooled": head, **sub}
         print(json.dumps(line), flush=True)
     dist.destroy_process_group()
 

@@ -35,3 +35,17 @@ def test_configs_names_checked_before_any_gpu_call():
     assert "unknown ['bogus']" in (r.stderr + r.stdout)
     r = _run(["--configs", "diamonds", "--gpus", "2"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
+
+
+def test_library_overrides_refused():
+    """Any AMH_* variable (a library path, the diagnostic build's A/B
+    switches) stops the bench before it touches a GPU: the line always
+    describes the release libamh.so."""
+    for var, val in (("AMH_S64_MOVE_ONLY", "1"), ("AMH_LIB_PATH", "/tmp/x.so"), ("AMH_STEP64", "0")):
+        r = _run(["--steps", "1", "--warmup", "0"], {var: val})
+        assert r.returncode != 0
+        assert f"unset {var}" in (r.stderr + r.stdout)
+    # the release library ignores the switches whatever the environment says
+    src = open(os.path.join(ROOT, "adaptive-mcmc_amd", "csrc", "amh_kernels.hip")).read()
+    i = src.index('getenv("AMH_S64_MOVE_ONLY")')
+    assert src.rfind("#ifdef AMH_DIAG", 0, i) > src.rfind("#endif", 0, i)

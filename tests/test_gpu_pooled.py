@@ -51,7 +51,7 @@ def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
     _run(kind, d, C, steps, gpu, orc)
 
 
-@pytest.mark.parametrize("d,C", [(16, 999), (128, 300), (256, 257)])
+@pytest.mark.parametrize("d,C", [(16, 999), (128, 300), (256, 257), (64, 70000), (64, 4097)])
 def test_pooled_inplace_multistep(d, C, gpu, orc):
     """sample_ (amh_pooled_step, in place: in and out states alias) equals
     repeated out-of-place sample(); covers the large-d update's staging."""
@@ -72,6 +72,46 @@ def test_pooled_inplace_multistep(d, C, gpu, orc):
     assert torch.equal(sa.adapt_state.loc, sb.adapt_state.loc) and torch.equal(sa.as_change, sb.as_change)
 
 
+@pytest.mark.parametrize("C,K,n", [(70000, 1, 3), (70000, 4, 8), (3000, 1, 5), (4097, 2, 6)])
+def test_pooled64_inplace_vs_oracle(C, K, n, gpu, orc):
+    """d = 64 in place (amh_pooled_step_k with the fused stats kernel and the
+    update launch that folds in the last step's chunk reduction: reduce blocks
+    write their sums write-through, take an agent-scope ticket, the last
+    arriver runs the update, accumulating over the K steps of a block).  C =
+    70,000 gives 547 chunks = 35 reduce groups (> 16).  Per-chain state, the
+    last block's sums (k._sums) and the shared state bit for bit against the
+    oracle's n / K blocks, and against n / K out-of-place sample() calls."""
+    from kernels_amd import PooledARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", 64)
+    z0 = np.random.default_rng(11).uniform(-2, 2, size=(C, 64)).astype(np.float32)
+    a = PooledARWMH(num_chains=C, sync_every=K, **kw)
+    sa = a.init(PRNGKey(11), 0, torch.as_tensor(z0), (), mk)
+    b = PooledARWMH(num_chains=C, sync_every=K, **kw)
+    sb = b.init(PRNGKey(11), 0, torch.as_tensor(z0), (), mk)
+    a.sample_(sa, n)
+    for _ in range(n // K):
+        sb = b.sample(sb)
+    ost = orc.init(om, PRNGKey(11), C, init_z=z0)
+    z, pe, keys = ost.z, ost.potential_energy, ost.rng_key
+    sh = orc.pooled_init_shared(64)
+    for _ in range(n // K):
+        z, pe, sums = orc.pooled_stats(om, int(sh["i"][0]), z, pe, keys, sh["mu"], sh["L"], float(sh["lam"][0]),
+                                       k_steps=K)
+        orc.pooled_update(om, sums, sh, k_steps=K)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a._sums.cpu().numpy().view(np.uint64), sums.view(np.uint64))
+    np.testing.assert_array_equal(b._sums.cpu().numpy().view(np.uint64), sums.view(np.uint64))
+    for st in (sa, sb):
+        got = dict(z=st.z, pe=st.potential_energy, mu=st.adapt_state.loc, L=st.adapt_state.scale,
+                   lam=st.adapt_state.log_step_size, macc=st.mean_accept_prob, asc=st.as_change, cov=st.cov, i=st.i)
+        want = dict(z=z, pe=pe, mu=sh["mu"], L=sh["L"], lam=sh["lam"], macc=sh["macc"], asc=sh["asc"],
+                    cov=sh["cov"], i=sh["i"])
+        for f in got:
+            g = got[f].cpu().numpy()
+            assert g.tobytes() == np.asarray(want[f]).astype(g.dtype).tobytes(), f"{f} differs (C={C} K={K})"
+    assert int(sa.i[0]) == n
+
+
 @pytest.mark.parametrize("kind,d,C,blocks,K", [("gaussian", 64, 3000, 3, 4), ("gaussian", 64, 70000, 2, 16),
                                                ("gaussian", 7, 517, 3, 5), ("eight_schools", None, 64, 3, 16),
                                                ("diamonds", None, 40, 2, 3), ("diamonds_ss", None, 1000, 2, 4),
@@ -83,7 +123,7 @@ def test_pooled_blocks_bitexact(kind, d, C, blocks, K, gpu, orc):
     _run(kind, d, C, blocks, gpu, orc, K=K)
 
 
-@pytest.mark.parametrize("d,C,K", [(16, 999, 4), (128, 300, 3)])
+@pytest.mark.parametrize("d,C,K", [(16, 999, 4), (128, 300, 3), (64, 70000, 4), (64, 70000, 1)])
 def test_pooled_blocks_inplace(d, C, K, gpu, orc):
     """sample_(12) with sync_every = K in place (amh_pooled_step_k) equals
     12 / K out-of-place block samples."""
@@ -101,8 +141,9 @@ def test_pooled_blocks_inplace(d, C, K, gpu, orc):
     assert int(sa.i[0]) == 12 and int(sb.i[0]) == 12
     assert torch.equal(sa.z, sb.z) and torch.equal(sa.adapt_state.scale, sb.adapt_state.scale)
     assert torch.equal(sa.cov, sb.cov) and torch.equal(sa.adapt_state.loc, sb.adapt_state.loc)
-    with pytest.raises(ValueError):
-        a.sample_(sa, 5 if K != 5 else 7)
+    if K > 1:
+        with pytest.raises(ValueError):
+            a.sample_(sa, 5 if K != 5 else 7)
 
 
 @pytest.mark.parametrize("kind,d,C,blocks,K", [("gaussian", 64, 3000, 5, 1), ("gaussian", 64, 2000, 4, 4),

@@ -17,5 +17,5 @@ timeout -k 10 120 python3 tools/pooled_run.py 65536 64 400 > $O/pool_plain.log 2
 timeout -k 10 120 python3 tools/pooled_run.py 32768 256 100 > $O/pool256.log 2>&1 && grep pooled $O/pool256.log || exit 9
 timeout -k 10 120 python3 tools/f64_stamps.py > $O/stamps.txt 2>&1; grep -v amdgpu.ids $O/stamps.txt
 # A/B: no noise drawn ahead (the update launch's own path alone)
-AMH_POOLED_NOISE_AHEAD=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/pool_nonoise -o run --output-format csv -- python3 tools/pooled_run.py 65536 64 200 > $O/pool_nonoise.log 2>&1; grep pooled $O/pool_nonoise.log
+AMH_LIB_PATH=adaptive-mcmc_amd/lib/diag/libamh_stamps.so AMH_POOLED_NOISE_AHEAD=0 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/pool_nonoise -o run --output-format csv -- python3 tools/pooled_run.py 65536 64 200 > $O/pool_nonoise.log 2>&1; grep pooled $O/pool_nonoise.log
 exit $rc

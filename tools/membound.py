@@ -11,6 +11,8 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "adaptive-mcmc_amd"))
+# the move-only switch exists in the diagnostic build only (make stamps)
+os.environ.setdefault("AMH_LIB_PATH", os.path.join(ROOT, "adaptive-mcmc_amd", "lib", "diag", "libamh_stamps.so"))
 
 
 def timeit(fn, n=50, warm=100):
@@ -38,13 +40,13 @@ def main():
         k.sample_(st, 3)
         ms = timeit(lambda: k.sample_(st, 1))
         print(f"{os.environ.get('AMH_S64_MOVE_ONLY', '0') == '1' and 'move-only' or 'step'}: {ms:.4f} ms "
-              f"-> {65536 * 17712 / ms / 1e9:.0f} GB/s algorithmic", flush=True)
+              f"-> {65536 * 17712 / ms / 1e9:.2f} TB/s algorithmic", flush=True)
         return
     nbytes = 65536 * 17712 // 2
     src = torch.empty(nbytes // 4, dtype=torch.float32, device="cuda").uniform_()
     dst = torch.empty_like(src)
     ms = timeit(lambda: dst.copy_(src))
-    print(f"torch copy {nbytes / 1e6:.0f} MB: {ms:.4f} ms -> {2 * nbytes / ms / 1e9:.0f} GB/s (read + write)", flush=True)
+    print(f"torch copy {nbytes / 1e6:.0f} MB: {ms:.4f} ms -> {2 * nbytes / ms / 1e9:.2f} TB/s (read + write)", flush=True)
     del src, dst
     for mo in ("1", "0"):
         r = subprocess.run([sys.executable, __file__, "step"], env=dict(os.environ, AMH_S64_MOVE_ONLY=mo),
