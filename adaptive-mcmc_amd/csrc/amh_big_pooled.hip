@@ -907,62 +907,51 @@ __device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, i
   });
 }
 
-// sqrtf(x) and then n / sqrtf(x), spelled out as the compiler's IEEE
-// expansions for gfx950 with f32 denormals on (v_sqrt_f32 + the +-1 ulp
-// residual correction, 2^32 pre-scaling below 2^-96, the zero/+inf class
-// select; v_div_scale / v_rcp / Newton fmas / v_div_fmas / v_div_fixup) --
-// the same instructions in the same order, so the same bits as `sqrtf` and
-// `/` (the oracle's operations).  fill(S), S = 0..15, runs after step S with a
-// scheduling barrier on both sides: independent work placed in the chain's
-// dependency stalls (an in-order wave cannot reorder it there by itself, and
-// the compiler's scheduler does not).
+// The shared factor's column k: y = amh_rsqrt_nr(x) (three Newton steps from
+// the bit-pattern seed, include/amh_math.h), L_kk = x y and q = n y -- the
+// oracle's operations in the same order, so the same bits.  Eleven dependent
+// VALU operations (the IEEE sqrtf + division expansions were about 30 and set
+// the factorisation's pivot-chain latency).  fill(S), S = 0..15, runs between
+// the chain's steps with a scheduling barrier on both sides: independent work
+// (the previous column's updates) placed in the chain's dependency stalls,
+// which an in-order wave cannot fill by itself.
 template <class F>
-__device__ __forceinline__ void ieee_sqrt_div(float x0, float n, float& sq, float& qt, F&& fill) {
-  using I = std::integral_constant<int, 0>;
+__device__ __forceinline__ void nr_sqrt_div(float x, float n, float& sq, float& qt, F&& fill) {
   auto step = [&](auto S) {
     __builtin_amdgcn_sched_barrier(0);
     fill(S);
     __builtin_amdgcn_sched_barrier(0);
   };
-  const bool sc = x0 < 0x1p-96f;
-  const float x = sc ? x0 * 0x1p32f : x0;
-  step(std::integral_constant<int, 0>{});
-  float r = __builtin_amdgcn_sqrtf(x);
-  step(std::integral_constant<int, 1>{});
-  const float rm = __int_as_float(__float_as_int(r) - 1), rp = __int_as_float(__float_as_int(r) + 1);
-  step(std::integral_constant<int, 2>{});
-  const float vp = fmaf(-rm, r, x);
-  step(std::integral_constant<int, 3>{});
-  const float vs = fmaf(-rp, r, x);
-  step(std::integral_constant<int, 4>{});
-  r = (vp <= 0.0f) ? rm : r;
-  r = (vs > 0.0f) ? rp : r;
-  step(std::integral_constant<int, 5>{});
-  r = sc ? r * 0x1p-16f : r;
-  const float s = __builtin_amdgcn_classf(x, 0x260) ? x : r;  // +-0, +inf
-  sq = s;
-  step(std::integral_constant<int, 6>{});
-  bool flag = false, unused = false;
-  const float den = __builtin_amdgcn_div_scalef(n, s, false, &unused);
-  const float num = __builtin_amdgcn_div_scalef(n, s, true, &flag);
-  step(std::integral_constant<int, 7>{});
-  const float rc = __builtin_amdgcn_rcpf(den);
-  step(std::integral_constant<int, 8>{});
-  const float f0 = fmaf(-den, rc, 1.0f);
-  step(std::integral_constant<int, 9>{});
-  const float f1 = fmaf(f0, rc, rc);
-  step(std::integral_constant<int, 10>{});
-  const float mu = num * f1;
-  step(std::integral_constant<int, 11>{});
-  const float f2 = fmaf(-den, mu, num);
-  step(std::integral_constant<int, 12>{});
-  const float f3 = fmaf(f2, f1, mu);
-  step(std::integral_constant<int, 13>{});
-  const float f4 = fmaf(-den, f3, num);
-  step(std::integral_constant<int, 14>{});
-  qt = __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(f4, f1, f3, flag), s, n);
-  step(std::integral_constant<int, 15>{});
-  (void)sizeof(I);
+  using namespace std;
+  const float h = 0.5f * x;
+  float y = __uint_as_float(0x5F375A86u - (__float_as_uint(x) >> 1));
+  step(integral_constant<int, 0>{});
+  float t = y * y;
+  step(integral_constant<int, 1>{});
+  t = fmaf(-h, t, 1.5f);
+  step(integral_constant<int, 2>{});
+  y = y * t;
+  step(integral_constant<int, 3>{});
+  t = y * y;
+  step(integral_constant<int, 4>{});
+  t = fmaf(-h, t, 1.5f);
+  step(integral_constant<int, 5>{});
+  y = y * t;
+  step(integral_constant<int, 6>{});
+  t = y * y;
+  step(integral_constant<int, 7>{});
+  t = fmaf(-h, t, 1.5f);
+  step(integral_constant<int, 8>{});
+  y = y * t;
+  step(integral_constant<int, 9>{});
+  sq = x * y;
+  qt = n * y;
+  step(integral_constant<int, 10>{});
+  step(integral_constant<int, 11>{});
+  step(integral_constant<int, 12>{});
+  step(integral_constant<int, 13>{});
+  step(integral_constant<int, 14>{});
+  step(integral_constant<int, 15>{});
 }
 
 template <int NT>
@@ -1060,8 +1049,8 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     // (1) the panel's 32 columns, rows p0 .. d-1, in registers: wave v holds
     // the diagonal block's rows p0 + ii in lanes ii < 32 (every wave a copy,
     // so no wave waits for another) and the rows p0 + 32 (v + 1) + ii below
-    // it in lanes 32 + ii.  Column k: pivot from lane k, L_kk = sqrtf, the
-    // whole column divided, then column k's update of the panel's later
+    // it in lanes 32 + ii.  Column k: pivot from lane k, y = rsqrt_nr, the
+    // whole column scaled by y, then column k's update of the panel's later
     // columns with L_mk broadcast from lane m (v_readlane) -- per element the
     // oracle's fmaf chain in column order.  Lanes above the diagonal compute
     // values that are never used.
@@ -1093,13 +1082,13 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
         static_for<32>([&](auto K) {
           constexpr int k = K;
           const float piv = rdlane(a[k], k);
-          ok = ok && (piv > 0.0f) && amh_isfinite(piv);
-          // ljj = sqrtf(piv), q = a[k] / ljj as their IEEE expansions, with
-          // column k-1's updates of the panel's columns m >= k+1 (packed
-          // pairs (m, m + 1), m even; column k + 1 alone when odd) in the
-          // chain's stalls (ieee_sqrt_div; the same bits)
+          ok = ok && amh_pivot_ok(piv);
+          // ljj = piv y, q = a[k] y with y = amh_rsqrt_nr(piv), with column
+          // k-1's updates of the panel's columns m >= k+1 (packed pairs
+          // (m, m + 1), m even; column k + 1 alone when odd) in the chain's
+          // stalls (nr_sqrt_div; the oracle's bits)
           float ljj, q;
-          ieee_sqrt_div(piv, a[k], ljj, q, [&](auto Sl) {
+          nr_sqrt_div(piv, a[k], ljj, q, [&](auto Sl) {
             if constexpr (k >= 1) {
               constexpr int m0 = ((k + 1) % 2 == 0) ? k + 1 : k + 2;
               if constexpr (Sl == 0 && m0 != k + 1) a[k + 1] = fmaf(-am1, pv[(k + 1) / 4][(k + 1) % 4], a[k + 1]);
@@ -1239,7 +1228,7 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
 // lane = row offset), Sigma' = (1-g) Sigma + g S_dd / N is formed in double
 // and rounded into LDS row by row, then wave 0 factors it with lane r holding
 // row r in 64 registers: column k's pivot comes from lane k (v_readlane),
-// L_kk = sqrtf, the column is divided, column k's update of column k + 1
+// L_kk = piv y (y = amh_rsqrt_nr), the column scaled by y, column k's update of column k + 1
 // follows through v_readlane (the next pivot is then ready), and its update
 // of the columns beyond arrives through a 64-float LDS broadcast applied
 // after the next column's pivot and division (software-pipelined; per
@@ -1504,8 +1493,8 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // oracle's fmaf chain), whichever wave applies it: wave f first applies
   // the finished columns 0 .. 16 f - 1 of the earlier waves as they appear
   // in `cols` (LDS, all 64 kept; `done` counts the finished ones), then
-  // factors its own 16 columns.  Column k: pivot (v_readlane), the IEEE
-  // sqrtf / division chain with column k-1's updates of the block's later
+  // factors its own 16 columns.  Column k: pivot (v_readlane), the
+  // rsqrt_nr chain (nr_sqrt_div) with column k-1's updates of the block's later
   // columns in its stalls, column k's update of column k + 1 through
   // v_readlane (the next pivot ready), column k to `cols`.  Entries above
   // the diagonal are never operands of valid ones.
@@ -1553,9 +1542,9 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
       constexpr int j = J;
       const int k = c0 + j;
       const float piv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[j]), k));
-      ok = ok && (piv > 0.0f) && amh_isfinite(piv);
+      ok = ok && amh_pivot_ok(piv);
       float ljj, q;
-      ieee_sqrt_div(piv, a[j], ljj, q, [&](auto Sl) {
+      nr_sqrt_div(piv, a[j], ljj, q, [&](auto Sl) {
         // column k-1's updates of this block's columns m >= k + 1 (packed
         // pairs (m, m + 1), m - c0 even; column k + 1 alone when odd)
         if constexpr (j >= 1) {

@@ -778,6 +778,12 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   if (threadIdx.x == 0) tick[0] = 0.0f;
   __syncthreads();
   const auto mctx = M::prepare(p.model, D, lane_id());
+#ifdef AMH_STAMPS
+  // diagnostic build: per-wave start / end on the constant 100 MHz clock and
+  // the items taken (tools/s64_tail.py: how long the launch drains)
+  const unsigned long long st_start = __builtin_amdgcn_s_memrealtime();
+  int st_items = 0;
+#endif
 
   const int64_t C = p.C;
   const int64_t n_items = C;  // one chain per wave
@@ -1109,6 +1115,9 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     prev_upd = Gp::any(updated);
     item = nxt;
     nxt = nxt2;
+#ifdef AMH_STAMPS
+    ++st_items;
+#endif
   }
   if (prev >= 0) {
     int lane = lane_id();
@@ -1132,6 +1141,19 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
+#ifdef AMH_STAMPS
+  {
+    const unsigned long long st_end = __builtin_amdgcn_s_memrealtime();
+    const int64_t w = (int64_t)blockIdx.x * WPB + wave_in_block;
+    if (w < kStampWaves && lane_id() == 0) {
+      g_stamps[w * kStampSlots + 0] = st_start;
+      g_stamps[w * kStampSlots + 1] = st_end;
+      g_stamps[w * kStampSlots + 2] = (unsigned long long)st_items;
+      g_stamps[w * kStampSlots + 3] = (unsigned long long)blockIdx.x;
+      g_stamps[w * kStampSlots + 7] = 1;
+    }
+  }
+#endif
 }
 
 template <int WPB>

@@ -353,4 +353,28 @@ AMH_HD float amh_lr_gamma(int32_t n, float a) {
   return 1.0f / (float)na;
 }
 
+/* ---------------------------------------------- shared-factor pivot ---- */
+/* The pooled (shared) factorisation's column scaling (regime B, d >= 64):
+ * 1/sqrt(x) by three Newton steps from the bit-pattern seed (3.4 % ->
+ * 1.7e-3 -> 4.6e-6 -> rounding), in fmaf / mul only, so the device and the
+ * host give the same bits; L_kk = x * y and the column below is multiplied
+ * by y.  Eleven dependent operations in place of IEEE sqrtf followed by an
+ * IEEE division (about 30): the pivot chain is the factorisation's critical
+ * path.
+ * Callers accept only normal, finite pivots (amh_pivot_ok). */
+AMH_HD int amh_pivot_ok(float x) { return x >= 1.17549435e-38f && amh_isfinite(x); }
+AMH_HD float amh_rsqrt_nr(float x) {
+  const float h = 0.5f * x;
+  float y = amh_u2f(0x5F375A86u - (amh_f2u(x) >> 1));
+  float t = y * y;
+  t = fmaf(-h, t, 1.5f);
+  y = y * t;
+  t = y * y;
+  t = fmaf(-h, t, 1.5f);
+  y = y * t;
+  t = y * y;
+  t = fmaf(-h, t, 1.5f);
+  return y * t;
+}
+
 #endif /* AMH_MATH_H */

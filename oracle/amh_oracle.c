@@ -1256,9 +1256,10 @@ static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t
   int ok = 1;
   for (int j = 0; j < d && ok; ++j) {
     const float piv = A[j * d + j];
-    if (!(piv > 0.0f) || !amh_isfinite(piv)) { ok = 0; break; }
-    const float ljj = sqrtf(piv);
-    for (int r = j + 1; r < d; ++r) A[r * d + j] = A[r * d + j] / ljj;
+    if (!amh_pivot_ok(piv)) { ok = 0; break; }
+    const float y = amh_rsqrt_nr(piv); /* L_kk = piv y, column scaled by y (amh_math.h) */
+    const float ljj = piv * y;
+    for (int r = j + 1; r < d; ++r) A[r * d + j] = A[r * d + j] * y;
     A[j * d + j] = ljj;
     for (int k = j + 1; k < d; ++k)
       for (int r = k; r < d; ++r) A[r * d + k] = fmaf(-A[r * d + j], A[k * d + j], A[r * d + k]);

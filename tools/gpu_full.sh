@@ -12,7 +12,13 @@ O=gpurun_out/$TAG
 mkdir -p $O
 KX=()
 [ -n "$2" ] && KX=(-k "$2")
-timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread "${KX[@]}" > $O/pytest_gpu.log 2>&1
+# progress line every minute (the last finished test), so a long CPU-side
+# oracle check inside one test is not taken for a hang; every step below
+# still has its own time limit
+( while sleep 60; do echo "[$(date +%T)] $(tail -n 1 $O/pytest_gpu.log 2>/dev/null | cut -c1-120)"; done ) &
+HB=$!
+trap "kill $HB 2>/dev/null" EXIT
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread --durations=20 "${KX[@]}" > $O/pytest_gpu.log 2>&1
 rc=$?; echo "pytest rc=$rc"; grep -E "passed|failed|FAILED|Error" $O/pytest_gpu.log | tail -12
 [ $rc -eq 0 ] || exit $rc
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
