@@ -88,6 +88,10 @@ class PooledARWMH(ARWMH):
         self._comm = None
         self.sync_every = int(sync_every)
         self.overlap = bool(overlap)
+        # testing / profiling: run the multi-rank step (stats launch, the
+        # all-reduce on the side stream, update launch) even in a world of one
+        # rank, so the RCCL branch can be exercised and timed on one GPU
+        self.force_collective = False
 
     def _world(self) -> int:
         if not dist.is_available() or not dist.is_initialized():
@@ -151,7 +155,7 @@ class PooledARWMH(ARWMH):
         stream after the compute stream's work so far; returns the event the
         consumer waits on.  gloo (ranks sharing a device, CPU tests): done
         in place, host-synchronous; returns None."""
-        if self._world() == 1:
+        if self._world() == 1 and not (self.force_collective and dist.is_available() and dist.is_initialized()):
             return None
         if dist.get_backend(self._group) != "nccl":
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self._group)
@@ -258,7 +262,7 @@ class PooledARWMH(ARWMH):
         K = self.sync_every
         if int(n_steps) % K != 0:
             raise ValueError(f"n_steps ({n_steps}) must be a multiple of sync_every ({K})")
-        if self._world() == 1 and not self.overlap:
+        if self._world() == 1 and not self.overlap and not self.force_collective:
             L = _lib.lib()
             dev = state.z.device.index
             c = self._c(state)

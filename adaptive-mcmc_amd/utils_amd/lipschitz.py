@@ -23,7 +23,6 @@ values agree with the reference in distribution, not bit for bit.
 from __future__ import annotations
 
 import math
-import struct
 from typing import Callable
 
 import numpy as np
@@ -38,16 +37,28 @@ __all__ = ["spectral_norm", "SpectralNormDense", "LipschitzNN", "compute_wassers
 _THRESHOLD = 1e-10
 
 
+def _start_vector(W2: torch.Tensor) -> torch.Tensor:
+    """The power iteration's unit start vector for W2 (see spectral_norm)."""
+    seed = int(math.trunc(float(W2[0, 0].detach()))) & 0xFFFFFFFF
+    g = torch.Generator(device="cpu")
+    g.manual_seed(seed)
+    u = torch.randn(W2.shape[0], generator=g, dtype=W2.dtype).to(W2.device)
+    return u / torch.linalg.norm(u)
+
+
 def spectral_norm(W: torch.Tensor, num_power_iters: int = 10, eps: float = 1e-10) -> torch.Tensor:
     """W / max(sigma_max(W), 1) with sigma from power iteration (lipschitz.py:10-57);
     differentiable through the iteration as in the reference."""
     shape = W.shape
     W2 = W.reshape(shape[0], -1)
-    seed = struct.unpack("<I", struct.pack("<f", float(W2[0, 0].detach())))[0]  # fold_in(PRNGKey(0), W[0, 0])
-    g = torch.Generator(device="cpu")
-    g.manual_seed(seed)
-    u = torch.randn(W2.shape[0], generator=g, dtype=W.dtype).to(W.device)
-    u = u / torch.linalg.norm(u)
+    # the start vector: random.fold_in(random.PRNGKey(0), W[0, 0]) folds in
+    # jnp.uint32(W[0, 0]), i.e. the weight truncated to an integer -- 0 for
+    # every |W[0, 0]| < 1, so in the reference the power iteration starts from
+    # the SAME vector at every training step (and the ten iterations, which
+    # are differentiated through, under-estimate sigma in a way the optimiser
+    # can learn to use).  The same here: the seed is the truncated weight
+    # (two's complement for negative values), not its bit pattern.
+    u = _start_vector(W2)
     v = torch.zeros(W2.shape[1], dtype=W.dtype, device=W.device)
     for _ in range(num_power_iters):
         v = W2.T @ u

@@ -344,3 +344,20 @@ def test_pooled_keep_factor_when_not_pd(d, C, gpu, orc):
                            ("lam", st.adapt_state.log_step_size, sh["lam"])):
             a = a.cpu().numpy()
             assert a.tobytes() == np.asarray(b).astype(a.dtype).tobytes(), f"{name} differs at step {t + 1}"
+
+
+def test_rccl_branch_one_rank_bitexact():
+    """The RCCL exchange (pooled.py _allreduce: the side stream, the event the
+    compute stream waits on) in a 1-rank `nccl` group, forced on one GPU, is
+    bit-equal to the fused one-rank path (tools/rccl_one_rank.py, its own
+    process so this process keeps no process group)."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_one_rank.py"), "65536", "64", "20"],
+                       capture_output=True, text=True, timeout=240, env=env)
+    print(r.stdout[-2000:], r.stderr[-2000:])
+    assert r.returncode == 0
+    assert "bit-equal to the fused path" in r.stdout

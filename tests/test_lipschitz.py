@@ -115,3 +115,19 @@ def test_kernel_distance_1d_notebook_cell101(gpu):
           f"residual vs notebook {m - 0.544187:+.4f}")
     assert abs(m - 0.544187) < 0.15
     assert min(rhos) - 2 * sd <= 0.544187 <= max(rhos) + 2 * sd
+
+
+def test_power_iteration_start_is_fixed_like_fold_in():
+    """lipschitz.py:30 folds jnp.uint32(W[0, 0]) into PRNGKey(0): every weight
+    with |W[0, 0]| < 1 starts the power iteration from the same vector (the
+    same at every training step), a different integer part from another."""
+    g = torch.Generator().manual_seed(3)
+    W = torch.randn(32, 32, generator=g) * 0.2
+    starts = []
+    for w00 in (0.3, -0.7, 0.0, 0.999, 1.5, 2.2):
+        W[0, 0] = w00
+        starts.append(Lz._start_vector(W))
+    for u in starts[1:4]:
+        assert torch.equal(u, starts[0])
+    assert not torch.equal(starts[4], starts[0]) and not torch.equal(starts[5], starts[4])
+    assert float(torch.linalg.norm(starts[0])) == pytest.approx(1.0, rel=1e-6)
