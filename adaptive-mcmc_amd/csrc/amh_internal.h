@@ -174,6 +174,7 @@ int64_t pooled_scratch_rows(int64_t n_chunks);  // partials + group sums of pool
 hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float* pep, double* sums, hipStream_t s);
 hipError_t run_pooled_big_update(const PooledUpdateParams& p, hipStream_t s, bool sigma_ready = false);
 hipError_t run_asss_step(int model_id, const StepParams& p, hipStream_t s);  // amh_asss.hip
+hipError_t run_asss_step64(const StepParams& p, hipStream_t s);  // amh_kernels.hip (d = 64 Gaussian)
 hipError_t run_asss_pnx(int model_id, const AsssPnxParams& p, hipStream_t s);
 // evaluation metrics (amh_eval.hip)
 int64_t kernel_sum_blocks(int64_t n, int64_t m);

@@ -18,6 +18,7 @@
 // Bit spec: the arithmetic order here is mirrored exactly by the C oracle
 // oracle/amh_oracle.c; both compile with -ffp-contract=off and take every
 // transcendental from include/amh_math.h.  See DESIGN.md "bit spec".
+#include "amh_asss.h"
 #include "amh_device.h"
 
 #include <cstdlib>
@@ -79,8 +80,12 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
     const uint32_t vo = 4u * lane;
     const Buf b0(uniform_ptr(p.in.i + first), bytes);
     const Buf b1(uniform_ptr(p.in.potential_energy + first), bytes);
-    const Buf b2(uniform_ptr(p.in.mean_accept_prob + first), bytes);
-    const Buf b3(uniform_ptr(p.in.log_step_size + first), bytes);
+    // (ASSS states have no mean_accept_prob / log_step_size: an empty range, so
+    // those DMAs read zeros and touch no memory)
+    const Buf b2(p.in.mean_accept_prob ? uniform_ptr(p.in.mean_accept_prob + first) : p.in.i,
+                 p.in.mean_accept_prob ? bytes : 0u);
+    const Buf b3(p.in.log_step_size ? uniform_ptr(p.in.log_step_size + first) : p.in.i,
+                 p.in.log_step_size ? bytes : 0u);
     const Buf b4(uniform_ptr(p.in.as_change + first), bytes);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(b0.rs, to_lds(ws + 0 * CPW), 4, (int)vo, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(b1.rs, to_lds(ws + 1 * CPW), 4, (int)vo, 0, 0, 0);
@@ -766,7 +771,10 @@ __device__ __forceinline__ void s64_tie(T& a) { asm volatile("s_waitcnt lgkmcnt(
 template <class T>
 __device__ __forceinline__ void s64_tie(T& a, T& b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)); }
 
-template <int WPB>
+// kASSS: the same persistent data movement around one ASSS transition
+// (asss_transition, amh_asss.h; asss.py:197-251) instead of the ARWMH one --
+// the state is the same but for mean_accept_prob / log_step_size (absent).
+template <int WPB, bool kASSS = false>
 __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   constexpr int D = 64;
   constexpr uint32_t P = kS64P;
@@ -821,12 +829,14 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     if (r == 0) {
       p.out.i[c] = it;
       p.out.potential_energy[c] = pe;
-      p.out.mean_accept_prob[c] = macc;
-      p.out.log_step_size[c] = lam;
+      if constexpr (!kASSS) {
+        p.out.mean_accept_prob[c] = macc;
+        p.out.log_step_size[c] = lam;
+      }
       p.out.as_change[c] = asc;
       p.out.rng_key[2 * c] = k0;
       p.out.rng_key[2 * c + 1] = k1;
-      if (p.accept_count != nullptr) p.accept_count[c] = acc0 + nacc;
+      if (!kASSS && p.accept_count != nullptr) p.accept_count[c] = acc0 + nacc;
     }
   };
   // factor of chain `c` copied verbatim from the launch input (no step of this
@@ -909,7 +919,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       s64_wr(zm_a + (uint32_t)r * 4u, dl);
       s64_wr_off<256>(zm_a + (uint32_t)r * 4u, inv);
       dl = lnew;
-      acc0 = (p.accept_count != nullptr && r == 0) ? p.accept_count[item] : 0;
+      acc0 = (!kASSS && p.accept_count != nullptr && r == 0) ? p.accept_count[item] : 0;
     }
 
     // ---- swap: read item k's column j (lanes > j), write item k-1's column j
@@ -945,6 +955,10 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     nacc = 0;
     bool updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
+     if constexpr (kASSS) {
+      asss_transition<64, GaussianM, true>(p, U, dl, z, mu, pe, asc, updated, it, k0, k1, D, r, r, true, mctx, lds);
+      it += 1;
+     } else {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
       const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
       const float xi = amh_normal_from_bits(o.v[0]);
@@ -1103,6 +1117,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       macc = maccn;
       mu = mun;
       lam = lamn;
+     }
       if (p.col_z != nullptr || p.col_pe != nullptr) {
         if ((t + 1) % p.thinning == 0) {
           const int64_t kk = t / p.thinning;
@@ -1156,11 +1171,11 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
 #endif
 }
 
-template <int WPB>
+template <int WPB, bool kASSS = false>
 hipError_t launch_step64(const StepParams& p, hipStream_t s) {
   constexpr size_t shm = s64_lds_bytes();
   static_assert(shm <= 163840, "d = 64 step kernel: LDS budget");
-  auto kern = arwmh_step64_kernel<WPB>;
+  auto kern = arwmh_step64_kernel<WPB, kASSS>;
   int per_cu = 0;
   hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, WPB * 64, shm);
   if (e != hipSuccess) return e;
@@ -1297,6 +1312,10 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
   if (model_id == AMH_MODEL_DIAMONDS_SS && p.d == kDiamondsD) return launch_step<32, DiamondsSSM, false, kDiamondsD>(p, s);
   return dispatch(model_id, p.d, StepF{p, s});
 }
+// ASSS at the d = 64 Gaussian (amh_asss.hip run_asss_step): the persistent
+// LDS-staged kernel around the ASSS transition
+hipError_t run_asss_step64(const StepParams& p, hipStream_t s) { return launch_step64<kS64Waves, true>(p, s); }
+
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s) {
   return dispatch(model_id, p.d, InitF{p, s});
 }
