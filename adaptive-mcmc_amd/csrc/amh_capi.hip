@@ -240,6 +240,7 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_init: no model bound");
   if (!key || !state_ok(out) || num_chains < 1 || chain_offset < 0)
     return fail(h, AMH_EINVAL, "amh_init: bad arguments");
+  h->big_ready_C = -1;  // a kept proposal belongs to a state this call may overwrite
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_init/hipSetDevice");
   amh::InitParams p{};
@@ -361,8 +362,15 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
     // collection is per launch: step t keeps slot t / thinning when (t+1) % thinning == 0
     const int64_t C = num_chains;
     const size_t need = (size_t)C * (size_t)(p.d + 1) * sizeof(float);
+    const bool grown = need > h->split_bytes;
     int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_step/hipMalloc");
     if (rc != AMH_OK) return rc;
+    // READY / KEEP as for d > 64: the step pass of each transition forms the
+    // next one's proposal (so the factor is read once per transition); only
+    // the first transition of a call may need the propose pass
+    const bool ready = !grown && (flags & AMH_STEP_PROPOSAL_READY) && h->big_ready_C == C &&
+                       same_buffers(*in, h->big_ready_out);
+    const bool keep_next = (flags & AMH_STEP_KEEP_PROPOSAL) != 0;
     h->big_ready_C = -1;
     float* xprop = h->split_buf;
     float* peprop = h->split_buf + (size_t)C * p.d;
@@ -376,7 +384,8 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
       const int64_t k = t / p.thinning;
       q.col_z = (keep && p.col_z) ? p.col_z + (size_t)k * C * p.d : nullptr;
       q.col_pe = (keep && p.col_pe) ? p.col_pe + (size_t)k * C : nullptr;
-      e = amh::run_propose(q, xprop, (hipStream_t)stream);
+      q.xprop_next = (t + 1 < n_steps || keep_next) ? xprop : nullptr;
+      if (t == 0 && !ready) e = amh::run_propose(q, xprop, (hipStream_t)stream);
       if (e == hipSuccess) {
         amh::PotParams pp{xprop, peprop, C, p.d, h->model, h->xpack};
         e = amh::run_potential_lane(h->model_id, pp, (hipStream_t)stream);
@@ -384,6 +393,8 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
       if (e == hipSuccess) e = amh::run_step_ext(q, (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(h, e, "amh_step(split)");
     }
+    h->big_ready_C = keep_next ? C : -1;
+    h->big_ready_out = *out;
     return AMH_OK;
   }
   e = amh::run_step(h->model_id, p, (hipStream_t)stream);

@@ -39,6 +39,8 @@ struct StepParams {
   int32_t gamma_tab_n;
   ModelArgs model;
   const float* ext_pe;     // split path: U(z') per chain from the batched potential (n_steps == 1)
+  float* xprop_next;       // split path: the NEXT transition's proposal [C][d] (or null), formed as
+                           // the propose pass would form it from the stored state
 };
 
 struct InitParams {

@@ -499,6 +499,35 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         }
       }
     }
+    if constexpr (kExt) {
+      // split path: the next transition's proposal, exactly as propose_kernel
+      // forms it from the state this launch stores -- L = U diag(dl) if a step
+      // updated the factor (else the input factor, whose U these registers
+      // already are), reloaded as U = L / L_jj -- so the batched potential of
+      // the next launch can run without a propose pass over the factor
+      if (p.xprop_next != nullptr) {
+        const bool any_upd = Gp::any(updated);
+        const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
+        const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+        const float el = amh_expf(lam);
+        const float eta = dl * xi;
+        float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        static_for<DMAX>([&](auto J) {
+          constexpr int j = J;
+          if (j < d) {
+            const float un = (r == j) ? 1.0f
+                                      : ((r > j) ? (U[j] * Gp::template bcast<j>(dl)) * Gp::template bcast<j>(inv)
+                                                 : 0.0f);
+            a4[j & 3] = fmaf(any_upd ? un : U[j], Gp::template bcast<j>(eta), a4[j & 3]);
+          }
+          column_fence<j, 16>();
+        });
+        const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+        if (chain_ok && act) p.xprop_next[chain * d + r] = zp;
+      }
+    }
 
     prev = item;
     item = nxt;

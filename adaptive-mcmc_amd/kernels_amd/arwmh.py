@@ -129,7 +129,7 @@ class ARWMH:
         self._model_kwargs = None
         self._dim = None
         self.accept_count = None  # [C] int32 accepted proposals since init (diagnostic)
-        self.chain_proposals = True  # d > 64: reuse the step pass's next proposal across sample() calls
+        self.chain_proposals = True  # d > 64 / diamonds: reuse the step pass's next proposal across sample() calls
 
     @property
     def model(self):
@@ -273,8 +273,9 @@ class ARWMH:
                               self.accept_count.data_ptr() if self.accept_count is not None else None, thin)
         dev = sin.z.device.index
         flags = 0
-        if self._dim > 64 and self.chain_proposals and not any(t.is_inference() for t in self._leaves(sin)):
-            # d > 64: the step pass forms the next proposal (amh_step_chained).
+        if self._chained_path() and self.chain_proposals and not any(t.is_inference() for t in self._leaves(sin)):
+            # d > 64 and the literal diamonds model: the step pass forms the
+            # next proposal (amh_step_chained).
             # It is reused only for the very tensors the last call returned
             # (weak references: a dead one never matches, so recycled storage
             # cannot pass), unmodified since (torch's in-place version counters;
@@ -308,6 +309,15 @@ class ARWMH:
             if self._potential_fn is None:
                 raise RuntimeError("call init() (or get_init_adapt_state()) first")
             self._bind(0, {}, _device_index(self._device))
+
+    def _chained_path(self) -> bool:
+        """Paths whose step pass forms the next transition's proposal: d > 64
+        (amh_big.hip) and the literal diamonds model's split transition
+        (amh_split.hip; include/amh.h AMH_STEP_KEEP_PROPOSAL)."""
+        if self._dim > 64:
+            return True
+        mid = self._model.model_id if self._model is not None else self._potential_fn.model_id
+        return mid == _lib.AMH_MODEL_DIAMONDS and 3 <= self._dim <= 32
 
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""

@@ -125,9 +125,10 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
 int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
              int32_t n_steps, const amh_collect* collect, void* stream);
 
-/* amh_step with flags (64 < d <= 256; other shapes ignore them).  The step
- * pass of the large-d path forms the next transition's proposal while it
- * streams L' out; AMH_STEP_KEEP_PROPOSAL keeps the one after the last step in
+/* amh_step with flags (64 < d <= 256 and the literal diamonds model's split
+ * transition; other shapes ignore them).  The step pass of those paths forms
+ * the next transition's proposal while it streams L' out (so the factor is
+ * read once per transition); AMH_STEP_KEEP_PROPOSAL keeps the one after the last step in
  * the handle, and AMH_STEP_PROPOSAL_READY tells the next call that its `in` is
  * that unchanged output (same chains), so its propose pass is skipped.  The
  * handle drops a kept proposal whenever its scratch is used otherwise, and

@@ -271,13 +271,14 @@ def test_diamonds_suffstat_generic_k(gpu, orc):
     np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
 
 
-def test_big_dim_chained_proposal_invalidation(gpu, orc):
-    """d > 64 sample() reuses the proposal the previous step pass formed only
-    for the unchanged state it returned: an in-place edit of z between calls
-    (torch version counter) or a different state object forces the propose
-    pass, and every path stays bit-identical to the oracle."""
-    d, C = 128, 65
-    k, st, om, ost = _init("gaussian", C, gpu, orc, d=d, num_warmup=2)
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 128, 65), ("diamonds", None, 66)])
+def test_big_dim_chained_proposal_invalidation(kind, d, C, gpu, orc):
+    """d > 64 and the literal diamonds split path: sample() reuses the proposal
+    the previous step pass formed only for the unchanged state it returned: an
+    in-place edit of z between calls (torch version counter) or a different
+    state object forces the propose pass, and every path stays bit-identical
+    to the oracle."""
+    k, st, om, ost = _init(kind, C, gpu, orc, d=d, num_warmup=2)
     for t in range(3):
         st = k.sample(st, (), {})
         orc.step(om, ost, 1, num_warmup=2)
