@@ -516,10 +516,14 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         static_for<DMAX>([&](auto J) {
           constexpr int j = J;
           if (j < d) {
-            const float un = (r == j) ? 1.0f
-                                      : ((r > j) ? (U[j] * Gp::template bcast<j>(dl)) * Gp::template bcast<j>(inv)
-                                                 : 0.0f);
-            a4[j & 3] = fmaf(any_upd ? un : U[j], Gp::template bcast<j>(eta), a4[j & 3]);
+            // the broadcasts run with every lane of the group active (a
+            // broadcast under a lane-dependent branch would read an inactive
+            // source lane); then the load path's own masking
+            const float dj = Gp::template bcast<j>(dl);
+            const float ij = Gp::template bcast<j>(inv);
+            const float ej = Gp::template bcast<j>(eta);
+            const float un = set_one_at<G, j>(keep_above<G, j>((U[j] * dj) * ij, rr), rr);
+            a4[j & 3] = fmaf(any_upd ? un : U[j], ej, a4[j & 3]);
           }
           column_fence<j, 16>();
         });
@@ -730,6 +734,15 @@ constexpr int kS64Waves = AMH_S64_WAVES;
 #ifndef AMH_S64_PB
 #define AMH_S64_PB 8
 #endif
+#ifndef AMH_S64_STEAL
+#define AMH_S64_STEAL 0  // diagnostic variant: percent of the chains in a grid-wide tail pool
+#endif
+constexpr int kS64Steal = AMH_S64_STEAL;
+#if AMH_S64_STEAL
+// [0] the tail pool's next ticket, [1] waves finished; the last wave of a
+// launch resets both (one stream at a time: a diagnostic-build variant)
+__device__ unsigned int g_s64_pool[2];
+#endif
 constexpr int kS64EB = AMH_S64_EB;  // proposal: broadcast columns per LDS wait (16 or 8)
 constexpr int kS64PB = AMH_S64_PB;  // potential: columns per LDS wait (16 or 8)
 static_assert((kS64EB == 16 || kS64EB == 8) && (kS64PB == 16 || kS64PB == 8), "batch sizes");
@@ -840,15 +853,40 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   int64_t prev = -1;
   bool prev_upd = false;
 
-  const int64_t blk_lo = n_items * (int64_t)blockIdx.x / gridDim.x;
-  const int64_t blk_hi = n_items * ((int64_t)blockIdx.x + 1) / gridDim.x;
+  // kS64Steal > 0 (diagnostic variant): the blocks' static ranges cover the
+  // first n_static chains; a wave whose block range is spent draws the rest
+  // from a grid-wide pool (agent-scope atomic whose result is read only at
+  // the next hand-over, after the vmcnt(0) that waits for the DMA anyway)
+  const int64_t n_static = kS64Steal > 0 ? n_items - (n_items * kS64Steal) / 100 : n_items;
+  const int64_t blk_lo = n_static * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t blk_hi = n_static * ((int64_t)blockIdx.x + 1) / gridDim.x;
+  const int64_t kEnd = kS64Steal > 0 ? n_items : blk_hi;  // "no item" sentinel
+  constexpr int64_t kPending = -2;                         // pool ticket in flight
+  [[maybe_unused]] uint32_t graw = 0;                      // its raw value (lane 0)
   const uint32_t tk_addr = lds_addr(tick);
-  auto ticket = [&]() -> int64_t {
+  auto ticket_local = [&]() -> int64_t {
     uint32_t v = 0;
     if (lane_id() == 0) {
       asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tk_addr), "v"(1u) : "memory");
     }
     return blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
+  };
+  auto pool_decode = [&]() -> int64_t {
+    const int64_t t = n_static + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)graw);
+    return t < n_items ? t : n_items;
+  };
+  // deferred: may return kPending (decode at the next hand-over)
+  auto ticket = [&](bool defer) -> int64_t {
+    const int64_t t = ticket_local();
+    if constexpr (kS64Steal > 0) {
+      if (t >= blk_hi) {
+#if AMH_S64_STEAL
+        if (lane_id() == 0) graw = __hip_atomic_fetch_add(&g_s64_pool[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+        return defer ? kPending : pool_decode();
+      }
+    }
+    return t;
   };
 
   // z, loc and the scalars of chain `c` from registers
@@ -904,16 +942,19 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     });
   };
 
-  int64_t item = ticket();
-  int64_t nxt = item < blk_hi ? ticket() : blk_hi;
-  if (item < blk_hi) prefetch_item<64, false>(p, item, D, wb, lane_id());
-  for (; item < blk_hi;) {
+  int64_t item = ticket(false);
+  int64_t nxt = item < kEnd ? ticket(false) : kEnd;
+  if (item < kEnd) prefetch_item<64, false>(p, item, D, wb, lane_id());
+  for (; item < kEnd;) {
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
     const int r = lane;
     const uint32_t la = wb_a + (uint32_t)r * 4u;  // this lane's dword in the factor region
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): item k has landed
+    if constexpr (kS64Steal > 0) {
+      if (nxt == kPending) nxt = pool_decode();  // its atomic returned with the DMA
+    }
     // the hand-over phase (stores, LDS -> registers, the next DMA) at high
     // wave priority so the memory queue is re-armed before other waves'
     // compute: 239 -> 236 us per launch (tools/gpu_prio.sh A/B)
@@ -974,10 +1015,10 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     if (wr) flush_factor(prev);
 
     s64_wait();  // every LDS read of the buffer is done before the DMA refills it
-    int64_t nxt2 = blk_hi;
-    if (nxt < blk_hi) {
+    int64_t nxt2 = kEnd;
+    if (nxt < kEnd) {
       prefetch_item<64, false>(p, nxt, D, wb, lane);
-      nxt2 = ticket();
+      nxt2 = ticket(true);
     }
     __builtin_amdgcn_s_setprio(0);
 
@@ -1185,6 +1226,15 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
+#if AMH_S64_STEAL
+  if (lane_id() == 0) {  // the launch's last wave resets the pool for the next one
+    const unsigned total = gridDim.x * WPB;
+    if (__hip_atomic_fetch_add(&g_s64_pool[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+      __hip_atomic_store(&g_s64_pool[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&g_s64_pool[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#endif
 #ifdef AMH_STAMPS
   {
     const unsigned long long st_end = __builtin_amdgcn_s_memrealtime();
