@@ -39,8 +39,10 @@ def main():
     ap.add_argument("--pmc-warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=65536)
     ap.add_argument("--dim", type=int, default=64)
+    ap.add_argument("--src", default=None, help="run directory (default gpurun_out/prof_<tag>; tools/gpu_full.sh "
+                                                "writes gpurun_out/<tag>)")
     a = ap.parse_args()
-    src = os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
+    src = a.src or os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
 
