@@ -35,6 +35,9 @@ __all__ = ["spectral_norm", "SpectralNormDense", "LipschitzNN", "compute_wassers
            "compute_kernel_distance", "compute_kernel_distance_1d"]
 
 _THRESHOLD = 1e-10
+# diagnostics: when a list, _train appends (step, loss, clipped-gradient norm)
+# of every training step (tools/cell101.py logs the trajectory)
+TRAIN_LOG = None
 
 
 def _start_vector(W2: torch.Tensor) -> torch.Tensor:
@@ -145,6 +148,8 @@ def _train(model, loss_fn, rng_key, max_steps: int, lr: float):
             p.grad.clamp_(-1.0, 1.0)
             gn += float((p.grad ** 2).sum())
         grad_norm = gn
+        if TRAIN_LOG is not None:
+            TRAIN_LOG.append((it, float(loss.detach()), gn))
         opt.step()
     print(f"Train finished in {it} steps. Last gradient norm: {grad_norm}.")
     return key

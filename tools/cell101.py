@@ -22,7 +22,7 @@ from utils_amd import lipschitz as Lz  # noqa: E402
 
 
 def main():
-    n_keys = int(sys.argv[1]) if len(sys.argv) > 1 else 4
+    n_keys = int(sys.argv[1]) if len(sys.argv) > 1 else 8
     g = P.gaussian(np.zeros(1), cov=np.eye(1))
     k = ARWMH(potential_fn=g, num_chains=1)
     s_p = (torch.zeros(1), torch.ones(1, 1), torch.zeros(()))
@@ -34,6 +34,7 @@ def main():
     rhos = []
     for seed in range(n_keys):
         buf = io.StringIO()
+        Lz.TRAIN_LOG = []
         with contextlib.redirect_stdout(buf):
             rho, model, _ = Lz.compute_kernel_distance_1d(fp, fq, PRNGKey(seed), x, sample_batch_size=1000,
                                                           n_train_batches=1, n_eval_batches=1000, max_steps=1000,
@@ -42,8 +43,11 @@ def main():
             f = model(grid)
             lip = float((f[1:] - f[:-1]).abs().max() / (grid[1, 0] - grid[0, 0]))
         rhos.append(rho)
+        traj = {s_: (l_, g_) for s_, l_, g_ in Lz.TRAIN_LOG}
+        tr = " ".join(f"{s_}:{-traj[s_][0]:.3f}/{traj[s_][1]:.3g}" for s_ in (1, 10, 100, 300, 600, 1000) if s_ in traj)
         print(f"key {seed}: rho {rho:.4f}; {buf.getvalue().strip()}; Lipschitz constant of the trained f "
-              f"on [-8, 8]: {lip:.4f}", flush=True)
+              f"on [-8, 8]: {lip:.4f}; training ratio/grad-norm at steps {tr}", flush=True)
+        Lz.TRAIN_LOG = None
     print(f"rho mean {np.mean(rhos):.4f} sd {np.std(rhos, ddof=1):.4f} (notebook 0.544187)")
 
 

@@ -15,5 +15,5 @@ r=$?; echo "configs rc=$r"; cut -c1-300 $O/configs.jsonl; [ $r -eq 0 ] || exit $
 bash tools/gpu_pooled_pmc.sh ${1:-extra} || exit 9
 timeout -k 10 240 python3 -u tools/rccl_one_rank.py 65536 64 200 > $O/rccl.txt 2>&1
 r=$?; echo "rccl rc=$r"; grep -v amdgpu.ids $O/rccl.txt | tail -4; [ $r -eq 0 ] || exit $r
-timeout -k 10 600 python3 -u tools/cell101.py 4 > $O/cell101.txt 2>&1
+timeout -k 10 600 python3 -u tools/cell101.py 8 > $O/cell101.txt 2>&1
 r=$?; echo "cell101 rc=$r"; grep -v amdgpu.ids $O/cell101.txt; exit $r
