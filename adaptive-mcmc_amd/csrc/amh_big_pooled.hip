@@ -171,44 +171,11 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   f32x16 sacc = f32x16{};  // S_dd of the chunk so far (waves 0..2)
   float sd = 0.0f, sa = 0.0f;  // S_d (wave 3, lane = coordinate), S_a (wave 3 lane 0)
   int cnt = 0;
-  // the first sub-chunk's loads go out before the shared operands' (one
-  // memory latency in the prologue instead of two)
-  if (nmine > 0) {
-    load_sub(0);
-    load_pe(0);
-  }
-  // A operands in registers: lane (i, h) of MFMA m holds row 32 T + i, column 2 m + h
-  {
-    // unconditional loads in one batch (above the diagonal: the row's
-    // diagonal entry, replaced by 0 once loaded); P rows to LDS in fperm order
-    const int r = 32 * T + i;
-    float pv[16];
-    static_for<32>([&](auto M) {
-      const int k = 2 * M + h;
-      aL[M] = p.L[pk(d, r, k <= r ? k : r)];
-    });
-    static_for<16>([&](auto N) { pv[N] = p.model.data[d + ((tid >> 6) + 4 * (int)N) * d + (tid & 63)]; });
-    static_for<32>([&](auto M) {
-      if (2 * M + h > r) aL[M] = 0.0f;
-    });
-    static_for<16>([&](auto N) {
-      const int row = (tid >> 6) + 4 * N, k = tid & 63;
-      lds[f64::PP + row * kFS + fperm(k)] = pv[N];
-    });
-    if (tid < d) {
-      lds[f64::MP + fperm(tid)] = p.model.data[tid];
-      lds[f64::MN + tid] = p.model.data[tid];
-    }
-  }
-  if (nmine > 0) store_z();
-  lds_barrier();
-  FS(14)
-  for (int64_t t = 0; t < nmine; ++t) {
-    const int64_t c0 = sub_c0(t);
-    const int64_t left = p.C - c0;
-    const int nv = left < kFSub ? (int)left : kFSub;
-    // ---- (1) noise of chains w + 4 N: drawn ahead by the previous update
-    // launch when the chain's record is this draw's (i, key), else here
+  // ---- (1) noise of chains w + 4 N of sub-chunk t: drawn ahead by the
+  // previous update launch when the chain's record is this draw's (i, key),
+  // else here.  PRE: the rows are already in xr0 (sub-chunk 0: the prologue)
+  float xr0[16];
+  auto noise_phase = [&](int64_t c0, auto PRE) {
     uint64_t usem = 0;
     if (ahead) {
       // lane N < 16: key word 0 of chain N is its own kr, word 1 lane N + 16's
@@ -219,9 +186,13 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     if (usem == 0xFFFFull) {  // every chain of the wave: rows of the buffer (one latency)
       float xr[16];
       static_for<16>([&](auto N) {
-        int64_t ch = c0 + w + 4 * N;
-        if (ch >= p.C) ch = p.C - 1;
-        xr[N] = p.xi[ch * d + lane];
+        if constexpr (decltype(PRE)::value) {
+          xr[N] = xr0[N];
+        } else {
+          int64_t ch = c0 + w + 4 * N;
+          if (ch >= p.C) ch = p.C - 1;
+          xr[N] = p.xi[ch * d + lane];
+        }
       });
       static_for<16>([&](auto N) {
         const int cc = w + 4 * N;
@@ -247,6 +218,54 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
         __builtin_amdgcn_sched_barrier(0);  // one chain at a time (the rare path: keeps registers for the rest)
       });
     }
+  };
+  // the first sub-chunk's loads -- z, keys, records, pe and (speculatively)
+  // its noise rows -- go out before the shared operands' (one memory latency
+  // in the prologue instead of three)
+  if (nmine > 0) {
+    load_sub(0);
+    load_pe(0);
+    const int64_t c00 = sub_c0(0);
+    static_for<16>([&](auto N) {
+      int64_t ch = c00 + w + 4 * N;
+      if (ch >= p.C) ch = p.C - 1;
+      xr0[N] = (ahead && ch < p.xi_cap) ? p.xi[ch * d + lane] : 0.0f;
+    });
+  }
+  // A operands in registers: lane (i, h) of MFMA m holds row 32 T + i, column 2 m + h
+  {
+    // unconditional loads in one batch (above the diagonal: the row's
+    // diagonal entry, replaced by 0 once loaded); P rows to LDS in fperm order
+    const int r = 32 * T + i;
+    float pv[16];
+    static_for<32>([&](auto M) {
+      const int k = 2 * M + h;
+      aL[M] = p.L[pk(d, r, k <= r ? k : r)];
+    });
+    static_for<16>([&](auto N) { pv[N] = p.model.data[d + ((tid >> 6) + 4 * (int)N) * d + (tid & 63)]; });
+    static_for<32>([&](auto M) {
+      if (2 * M + h > r) aL[M] = 0.0f;
+    });
+    static_for<16>([&](auto N) {
+      const int row = (tid >> 6) + 4 * N, k = tid & 63;
+      lds[f64::PP + row * kFS + fperm(k)] = pv[N];
+    });
+    if (tid < d) {
+      lds[f64::MP + fperm(tid)] = p.model.data[tid];
+      lds[f64::MN + tid] = p.model.data[tid];
+    }
+  }
+  if (nmine > 0) {
+    store_z();
+    noise_phase(sub_c0(0), std::true_type{});  // sub-chunk 0's phase (1), its rows already loaded
+  }
+  lds_barrier();
+  FS(14)
+  for (int64_t t = 0; t < nmine; ++t) {
+    const int64_t c0 = sub_c0(t);
+    const int64_t left = p.C - c0;
+    const int nv = left < kFSub ? (int)left : kFSub;
+    if (t > 0) noise_phase(c0, std::false_type{});
     const bool more = t + 1 < nmine;
     if (more) load_sub(t + 1);  // in flight through phases (2) .. (6)
     FS(0)
