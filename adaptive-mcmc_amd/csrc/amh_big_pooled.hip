@@ -109,8 +109,13 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   constexpr int kSub = kFChunk / kFSub;  // sub-chunks per chunk
   const int64_t Vt = d + 3 * 1024 + 4;   // pooled_big_tile_V(64)
   float* Zs = lds + f64::Z_;
-  float* Xi = lds + f64::XI;
-  float* Xp = lds + f64::XP;
+  // the noise / delta tile and the proposal tile swap roles every sub-chunk:
+  // sub-chunk t + 1's noise is written into this sub-chunk's proposal tile
+  // during phase (6), once phase (5) has read it
+  float* const XA = lds + f64::XI;
+  float* const XB = lds + f64::XP;
+  float* Xi = XA;
+  float* Xp = XB;
   float* uu = lds + f64::U_;
   float* tsum = lds + f64::TS;
   int* flag = (int*)(lds + f64::FL);
@@ -261,11 +266,14 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   }
   lds_barrier();
   FS(14)
+  bool pre_ok = false;  // this sub-chunk's noise rows were written during the previous one
   for (int64_t t = 0; t < nmine; ++t) {
     const int64_t c0 = sub_c0(t);
     const int64_t left = p.C - c0;
     const int nv = left < kFSub ? (int)left : kFSub;
-    if (t > 0) noise_phase(c0, std::false_type{});
+    Xi = (t & 1) ? XB : XA;
+    Xp = (t & 1) ? XA : XB;
+    if (t > 0 && !pre_ok) noise_phase(c0, std::false_type{});
     const bool more = t + 1 < nmine;
     if (more) load_sub(t + 1);  // in flight through phases (2) .. (6)
     FS(0)
@@ -339,6 +347,21 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     FS(6)
     lds_barrier();
     FS(7)
+    // ---- the next sub-chunk's noise rows, loaded now (its records came with
+    // load_sub(t + 1) in phase (1)) and written to its tile in phase (6)
+    float xn[16];
+    bool pre_next = false;
+    if (more && ahead) {
+      const int64_t c1 = sub_c0(t + 1);
+      static_for<16>([&](auto N) {
+        int64_t ch = c1 + w + 4 * N;
+        if (ch >= p.C) ch = p.C - 1;
+        xn[N] = (ch < p.xi_cap) ? p.xi[ch * d + lane] : 0.0f;
+      });
+      const uint32_t kw1 = (uint32_t)__shfl_down((int)kr, 16, 64);
+      const bool ok = (lane < 16) && rec.x == (uint32_t)it && rec.y == kr && rec.z == kw1;
+      pre_next = __ballot(ok) == 0xFFFFull;
+    }
     // ---- (5) z' out, delta = z' - mu as [k][fperm chain] over the xi array
     //      (every LDS read first, then the stores)
     {
@@ -361,6 +384,15 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     FS(8)
     lds_barrier();
     FS(9)
+    if (pre_next) {  // the proposal tile is free now: sub-chunk t + 1's noise and u
+      static_for<16>([&](auto N) {
+        const int cc = w + 4 * N;
+        Xp[cc * kFS + fperm(lane)] = xn[N];
+        const uint32_t ub = (uint32_t)__builtin_amdgcn_readlane((int)rec.w, N);
+        if (lane == 0) uu[cc] = amh_unif01_from_bits(ub);
+      });
+    }
+    pre_ok = pre_next;
     // ---- (6) the chunk's sums, accumulated over its sub-chunks in chain order
     {
       const bool last = (t % kSub == kSub - 1) || !more;  // the chunk's last sub-chunk
