@@ -93,9 +93,14 @@ __device__ __forceinline__ void prefetch_item(const StepParams& p, int64_t first
     __builtin_amdgcn_raw_ptr_buffer_load_lds(b3.rs, to_lds(ws + 3 * CPW), 4, (int)vo, 0, 0, 0);
     __builtin_amdgcn_raw_ptr_buffer_load_lds(b4.rs, to_lds(ws + 4 * CPW), 4, (int)vo, 0, 0, 0);
   }
-  if (lane < 2 * CPW) {
+  {
+    // 2 CPW key words: two DMAs of 64 lanes when a wave holds 64 chains (G = 1)
     const Buf bk(uniform_ptr(p.in.rng_key + 2 * first), (uint32_t)nvalid * 8u);
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(bk.rs, to_lds(ws + 5 * CPW), 4, (int)(4u * lane), 0, 0, 0);
+    static_for<(2 * CPW + 63) / 64>([&](auto H) {
+      constexpr int o = 64 * H;
+      if (lane + o < 2 * CPW)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(bk.rs, to_lds(ws + 5 * CPW + o), 4, (int)(4u * (lane + o)), 0, 0, 0);
+    });
   }
   if (EXT && lane < CPW) {  // split path: U(z') of the batched potential kernel
     const Buf be(uniform_ptr(p.ext_pe + first), (uint32_t)nvalid * 4u);
@@ -855,37 +860,29 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
 
   // kS64Steal > 0 (diagnostic variant): the blocks' static ranges cover the
   // first n_static chains; a wave whose block range is spent draws the rest
-  // from a grid-wide pool (agent-scope atomic whose result is read only at
-  // the next hand-over, after the vmcnt(0) that waits for the DMA anyway)
+  // from a grid-wide pool (agent-scope atomic).  The draw is made before the
+  // next DMA is issued, so a pool draw (the tail only) waits for the
+  // hand-over's stores but never for the prefetch, and no value of it stays
+  // live across the compute phase (the kernel is at its VGPR budget)
   const int64_t n_static = kS64Steal > 0 ? n_items - (n_items * kS64Steal) / 100 : n_items;
   const int64_t blk_lo = n_static * (int64_t)blockIdx.x / gridDim.x;
   const int64_t blk_hi = n_static * ((int64_t)blockIdx.x + 1) / gridDim.x;
   const int64_t kEnd = kS64Steal > 0 ? n_items : blk_hi;  // "no item" sentinel
-  constexpr int64_t kPending = -2;                         // pool ticket in flight
-  [[maybe_unused]] uint32_t graw = 0;                      // its raw value (lane 0)
   const uint32_t tk_addr = lds_addr(tick);
-  auto ticket_local = [&]() -> int64_t {
+  auto ticket = [&]() -> int64_t {
     uint32_t v = 0;
     if (lane_id() == 0) {
       asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tk_addr), "v"(1u) : "memory");
     }
-    return blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-  };
-  auto pool_decode = [&]() -> int64_t {
-    const int64_t t = n_static + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)graw);
-    return t < n_items ? t : n_items;
-  };
-  // deferred: may return kPending (decode at the next hand-over)
-  auto ticket = [&](bool defer) -> int64_t {
-    const int64_t t = ticket_local();
-    if constexpr (kS64Steal > 0) {
-      if (t >= blk_hi) {
+    int64_t t = blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
 #if AMH_S64_STEAL
-        if (lane_id() == 0) graw = __hip_atomic_fetch_add(&g_s64_pool[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
-        return defer ? kPending : pool_decode();
-      }
+    if (t >= blk_hi) {
+      uint32_t g = 0;
+      if (lane_id() == 0) g = __hip_atomic_fetch_add(&g_s64_pool[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      t = n_static + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)g);
+      if (t > kEnd) t = kEnd;
     }
+#endif
     return t;
   };
 
@@ -942,8 +939,8 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     });
   };
 
-  int64_t item = ticket(false);
-  int64_t nxt = item < kEnd ? ticket(false) : kEnd;
+  int64_t item = ticket();
+  int64_t nxt = item < kEnd ? ticket() : kEnd;
   if (item < kEnd) prefetch_item<64, false>(p, item, D, wb, lane_id());
   for (; item < kEnd;) {
     int lane = lane_id();
@@ -952,9 +949,6 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     const uint32_t la = wb_a + (uint32_t)r * 4u;  // this lane's dword in the factor region
 
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): item k has landed
-    if constexpr (kS64Steal > 0) {
-      if (nxt == kPending) nxt = pool_decode();  // its atomic returned with the DMA
-    }
     // the hand-over phase (stores, LDS -> registers, the next DMA) at high
     // wave priority so the memory queue is re-armed before other waves'
     // compute: 239 -> 236 us per launch (tools/gpu_prio.sh A/B)
@@ -1017,8 +1011,13 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     s64_wait();  // every LDS read of the buffer is done before the DMA refills it
     int64_t nxt2 = kEnd;
     if (nxt < kEnd) {
-      prefetch_item<64, false>(p, nxt, D, wb, lane);
-      nxt2 = ticket(true);
+      if constexpr (kS64Steal > 0) {
+        nxt2 = ticket();  // (a pool draw waits here for this hand-over's stores, not for the DMA)
+        prefetch_item<64, false>(p, nxt, D, wb, lane);
+      } else {
+        prefetch_item<64, false>(p, nxt, D, wb, lane);
+        nxt2 = ticket();
+      }
     }
     __builtin_amdgcn_s_setprio(0);
 

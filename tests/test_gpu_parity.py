@@ -47,7 +47,7 @@ def test_potential_bitexact(kind, d, gpu, orc):
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("gaussian", 7, 517), ("gaussian", 32, 300),
                                       ("eight_schools", None, 400), ("kidiq", None, 257),
                                       ("diamonds", None, 66), ("diamonds_ss", None, 333), ("mixture", 1, 1000),
-                                      ("mixture", 5, 300)])
+                                      ("mixture", 5, 300), ("gaussian", 1, 1000), ("gaussian", 2, 333)])
 def test_single_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.sample (one launch per step) vs oracle step(n_steps=1), 40 steps."""
     k, st, om, ost = _init(kind, C, gpu, orc, d=d, num_warmup=10)
@@ -60,7 +60,7 @@ def test_single_steps_bitexact(kind, d, C, gpu, orc):
     np.testing.assert_array_equal(k.accept_count.cpu().numpy(), acc)
 
 
-@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 2000), ("eight_schools", None, 1000),
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 2000), ("eight_schools", None, 1000), ("gaussian", 1, 777),
                                       ("diamonds", None, 130), ("diamonds_ss", None, 1000)])
 def test_fused_steps_bitexact(kind, d, C, gpu, orc):
     """ARWMH.run (n steps in one launch, z collected) vs oracle step(n_steps)."""
