@@ -53,9 +53,12 @@ __device__ __forceinline__ void asss_transition(const StepParams& p, float (&U)[
   const float zd = (ns - 1.0f) / den;
 
   // ---- v orthogonal to z on S^d (asss.py:219-222)
+  // v - (v.z) z with one rounding per component (fmaf): with the product
+  // rounded first, a draw numerically parallel to z (about 1e-9 per
+  // transition at d = 1) cancelled to exactly 0 and v / |v| was NaN
   const float dot = Gp::sum(act ? v * zr : 0.0f) + (vd * zd);
-  v = act ? v - dot * zr : 0.0f;
-  vd = vd - dot * zd;
+  v = act ? fmaf(-dot, zr, v) : 0.0f;
+  vd = fmaf(-dot, zd, vd);
   const float nv = sqrtf(Gp::sum(v * v) + (vd * vd));
   v = v / nv;
   vd = vd / nv;

@@ -1228,7 +1228,9 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
 #if AMH_S64_STEAL
   if (lane_id() == 0) {  // the launch's last wave resets the pool for the next one
     const unsigned total = gridDim.x * WPB;
-    if (__hip_atomic_fetch_add(&g_s64_pool[1], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
+    // relaxed: the kernel boundary orders the reset before the next launch (an
+    // agent-scope release here would write back the L2 in every wave)
+    if (__hip_atomic_fetch_add(&g_s64_pool[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
       __hip_atomic_store(&g_s64_pool[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(&g_s64_pool[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

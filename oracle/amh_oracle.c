@@ -1345,8 +1345,8 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
   /* v on the tangent space of z, normalised (asss.py:219-222) */
   for (int r = 0; r < G; ++r) t[r] = (r < d) ? v[r] * zr[r] : 0.0f;
   const float dot = group_sum(t, G) + (vd * zd);
-  for (int r = 0; r < d; ++r) v[r] = v[r] - dot * zr[r];
-  vd = vd - dot * zd;
+  for (int r = 0; r < d; ++r) v[r] = fmaf(-dot, zr[r], v[r]); /* one rounding: no exact cancellation */
+  vd = fmaf(-dot, zd, vd);
   for (int r = 0; r < G; ++r) t[r] = (r < d) ? v[r] * v[r] : 0.0f;
   const float nv = sqrtf(group_sum(t, G) + (vd * vd));
   for (int r = 0; r < d; ++r) v[r] = v[r] / nv;
