@@ -24,6 +24,15 @@
 
 namespace amh {
 
+// memory order of the cross-block arrival tickets (acquire-release; the
+// diagnostic variant -DAMH_TICKET_RELAXED measures what the release's L2
+// write-back and the acquire's invalidate cost)
+#ifdef AMH_TICKET_RELAXED
+#define AMH_TICKET_ORDER __ATOMIC_RELAXED
+#else
+#define AMH_TICKET_ORDER __ATOMIC_ACQ_REL
+#endif
+
 namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kLd = 65;          // LDS row stride of [k][chain] tiles
@@ -1465,7 +1474,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
     // acquire-release at agent scope: this block's sums are released with the
     // ticket and the last arriver acquires every other block's
-    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, AMH_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
     if (tk != nred - 1) {  // not the last: a noise worker
       if (nlate == 0) return;
@@ -1755,7 +1764,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
     const float cs = (wsum[0] + wsum[1]) + (wsum[2] + wsum[3]);
     __hip_atomic_store(&colsum[k], __float_as_uint(cs), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    last = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) == d - 1;
+    last = __hip_atomic_fetch_add(ticket, 1, AMH_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT) == d - 1;
   }
   __syncthreads();
   if (!last) return;
