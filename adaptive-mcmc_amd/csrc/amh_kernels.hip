@@ -739,15 +739,6 @@ constexpr int kS64Waves = AMH_S64_WAVES;
 #ifndef AMH_S64_PB
 #define AMH_S64_PB 8
 #endif
-#ifndef AMH_S64_STEAL
-#define AMH_S64_STEAL 0  // diagnostic variant: percent of the chains in a grid-wide tail pool
-#endif
-constexpr int kS64Steal = AMH_S64_STEAL;
-#if AMH_S64_STEAL
-// [0] the tail pool's next ticket, [1] waves finished; the last wave of a
-// launch resets both (one stream at a time: a diagnostic-build variant)
-__device__ unsigned int g_s64_pool[2];
-#endif
 constexpr int kS64EB = AMH_S64_EB;  // proposal: broadcast columns per LDS wait (16 or 8)
 constexpr int kS64PB = AMH_S64_PB;  // potential: columns per LDS wait (16 or 8)
 static_assert((kS64EB == 16 || kS64EB == 8) && (kS64PB == 16 || kS64PB == 8), "batch sizes");
@@ -858,32 +849,16 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
   int64_t prev = -1;
   bool prev_upd = false;
 
-  // kS64Steal > 0 (diagnostic variant): the blocks' static ranges cover the
-  // first n_static chains; a wave whose block range is spent draws the rest
-  // from a grid-wide pool (agent-scope atomic).  The draw is made before the
-  // next DMA is issued, so a pool draw (the tail only) waits for the
-  // hand-over's stores but never for the prefetch, and no value of it stays
-  // live across the compute phase (the kernel is at its VGPR budget)
-  const int64_t n_static = kS64Steal > 0 ? n_items - (n_items * kS64Steal) / 100 : n_items;
-  const int64_t blk_lo = n_static * (int64_t)blockIdx.x / gridDim.x;
-  const int64_t blk_hi = n_static * ((int64_t)blockIdx.x + 1) / gridDim.x;
-  const int64_t kEnd = kS64Steal > 0 ? n_items : blk_hi;  // "no item" sentinel
+  const int64_t blk_lo = n_items * (int64_t)blockIdx.x / gridDim.x;
+  const int64_t blk_hi = n_items * ((int64_t)blockIdx.x + 1) / gridDim.x;
+  const int64_t kEnd = blk_hi;  // "no item" sentinel
   const uint32_t tk_addr = lds_addr(tick);
   auto ticket = [&]() -> int64_t {
     uint32_t v = 0;
     if (lane_id() == 0) {
       asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(v) : "v"(tk_addr), "v"(1u) : "memory");
     }
-    int64_t t = blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
-#if AMH_S64_STEAL
-    if (t >= blk_hi) {
-      uint32_t g = 0;
-      if (lane_id() == 0) g = __hip_atomic_fetch_add(&g_s64_pool[0], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      t = n_static + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)g);
-      if (t > kEnd) t = kEnd;
-    }
-#endif
-    return t;
+    return blk_lo + (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)v);
   };
 
   // z, loc and the scalars of chain `c` from registers
@@ -1011,13 +986,8 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     s64_wait();  // every LDS read of the buffer is done before the DMA refills it
     int64_t nxt2 = kEnd;
     if (nxt < kEnd) {
-      if constexpr (kS64Steal > 0) {
-        nxt2 = ticket();  // (a pool draw waits here for this hand-over's stores, not for the DMA)
-        prefetch_item<64, false>(p, nxt, D, wb, lane);
-      } else {
-        prefetch_item<64, false>(p, nxt, D, wb, lane);
-        nxt2 = ticket();
-      }
+      prefetch_item<64, false>(p, nxt, D, wb, lane);
+      nxt2 = ticket();
     }
     __builtin_amdgcn_s_setprio(0);
 
@@ -1225,17 +1195,6 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     }
   }
   __builtin_amdgcn_s_waitcnt(0);
-#if AMH_S64_STEAL
-  if (lane_id() == 0) {  // the launch's last wave resets the pool for the next one
-    const unsigned total = gridDim.x * WPB;
-    // relaxed: the kernel boundary orders the reset before the next launch (an
-    // agent-scope release here would write back the L2 in every wave)
-    if (__hip_atomic_fetch_add(&g_s64_pool[1], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == total - 1) {
-      __hip_atomic_store(&g_s64_pool[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(&g_s64_pool[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-#endif
 #ifdef AMH_STAMPS
   {
     const unsigned long long st_end = __builtin_amdgcn_s_memrealtime();
