@@ -749,7 +749,8 @@ constexpr int kS64WB = kS64X + 64;            // floats per wave buffer (9,120 B
 constexpr int kS64Model = 64 * 68;            // GaussianM<64> rows (lds_bytes / 4)
 static_assert(kS64Z == 2080 && kS64S == kS64M + 64, "layout of prefetch_item<64>");
 // + 32 floats: the ticket, and slack for flush_factor's 9 KiB read of the last wave buffer
-constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)kS64Waves * kS64WB + 32) * sizeof(float); }
+template <int WPB = kS64Waves>
+constexpr size_t s64_lds_bytes() { return ((size_t)kS64Model + (size_t)WPB * kS64WB + 32) * sizeof(float); }
 
 constexpr int s64_col(int j) { return j * 64 - j * (j - 1) / 2; }  // packed column offset
 
@@ -1212,7 +1213,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
 
 template <int WPB, bool kASSS = false>
 hipError_t launch_step64(const StepParams& p, hipStream_t s) {
-  constexpr size_t shm = s64_lds_bytes();
+  constexpr size_t shm = s64_lds_bytes<WPB>();
   static_assert(shm <= 163840, "d = 64 step kernel: LDS budget");
   auto kern = arwmh_step64_kernel<WPB, kASSS>;
   int per_cu = 0;
@@ -1353,7 +1354,12 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
 }
 // ASSS at the d = 64 Gaussian (amh_asss.hip run_asss_step): the persistent
 // LDS-staged kernel around the ASSS transition
-hipError_t run_asss_step64(const StepParams& p, hipStream_t s) { return launch_step64<kS64Waves, true>(p, s); }
+#ifndef AMH_ASSS64_WAVES
+#define AMH_ASSS64_WAVES 12  // 170 VGPRs: the ASSS transition spilled 64 B at 16 waves (128 VGPRs)
+#endif
+hipError_t run_asss_step64(const StepParams& p, hipStream_t s) {
+  return launch_step64<AMH_ASSS64_WAVES, true>(p, s);
+}
 
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s) {
   return dispatch(model_id, p.d, InitF{p, s});
