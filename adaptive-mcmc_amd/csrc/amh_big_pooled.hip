@@ -33,6 +33,16 @@ namespace amh {
 #define AMH_TICKET_ORDER __ATOMIC_ACQ_REL
 #endif
 
+// fused stats kernel, drawn-ahead noise rows loaded early (diagnostic
+// variants; measured at C = 65,536, r4h): AMH_F64_PRE=1 loads sub-chunk 0's
+// with its z in the prologue, =2 also the next sub-chunk's during the current
+// one (phase (5), written in (6)): 31.5 us without, 33.9 us with both
+#ifndef AMH_F64_PRE
+#define AMH_F64_PRE 0
+#endif
+constexpr bool kF64Pre0 = AMH_F64_PRE >= 1;
+constexpr bool kF64Pre = AMH_F64_PRE >= 2;
+
 namespace {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 constexpr int kLd = 65;          // LDS row stride of [k][chain] tiles
@@ -240,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     load_sub(0);
     load_pe(0);
     const int64_t c00 = sub_c0(0);
-    static_for<16>([&](auto N) {
+    if constexpr (kF64Pre0) static_for<16>([&](auto N) {
       int64_t ch = c00 + w + 4 * N;
       if (ch >= p.C) ch = p.C - 1;
       xr0[N] = (ahead && ch < p.xi_cap) ? p.xi[ch * d + lane] : 0.0f;
@@ -271,7 +281,8 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   }
   if (nmine > 0) {
     store_z();
-    noise_phase(sub_c0(0), std::true_type{});  // sub-chunk 0's phase (1), its rows already loaded
+    if constexpr (kF64Pre0) noise_phase(sub_c0(0), std::true_type{});  // sub-chunk 0's phase (1), its rows already loaded
+    else noise_phase(sub_c0(0), std::false_type{});
   }
   lds_barrier();
   FS(14)
@@ -360,7 +371,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     // load_sub(t + 1) in phase (1)) and written to its tile in phase (6)
     float xn[16];
     bool pre_next = false;
-    if (more && ahead) {
+    if (kF64Pre && more && ahead) {
       const int64_t c1 = sub_c0(t + 1);
       static_for<16>([&](auto N) {
         int64_t ch = c1 + w + 4 * N;
@@ -913,10 +924,27 @@ __device__ unsigned long long g_upd_stamps[8];
 hipError_t diag_upd_stamps_copy(void* host) {
   return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_upd_stamps), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost);
 }
+// d = 64 update launch timeline on the 100 MHz constant clock (thread 0 of
+// each block; atomicMax of the value, or of ~value for a minimum): [0] ~first
+// block entry, [1] last reduce slice done, [2] ticket won, [3] Sigma' formed,
+// [4] factorisation done, [5] update end, [6] last noise worker end,
+// [7] ~first noise worker start.  Copied and cleared by amh_diag_u64_timeline.
+__device__ unsigned long long g_u64_rt[8];
+#define URT_MAX(k, v) \
+  if (threadIdx.x == 0) atomicMax(&g_u64_rt[k], (unsigned long long)(v));
+#define URT_NOW() __builtin_amdgcn_s_memrealtime()
+hipError_t diag_u64_timeline_copy(void* host) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_u64_rt), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  static const unsigned long long z[8] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_u64_rt), z, sizeof(z), 0, hipMemcpyHostToDevice);
+}
 #else
 #define US_INIT
 #define US(k)
 #define US_FLUSH
+#define URT_MAX(k, v)
+#define URT_NOW() 0ull
 #endif
 
 // LDS layout of the update ("A4"): column-major lower triangle where column j
@@ -1411,6 +1439,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // the noise position, read before any block can reach the update's write of
   // out.i (in place, in == out): a late reduce worker reads it in a register
   const int32_t inext = p.in.i[0] + p.K;
+  URT_MAX(0, ~URT_NOW())
   auto draw_noise = [&](int64_t worker, int64_t nworkers, int64_t cbeg, int64_t cend) {
     const int lane = lane_id();
     // wave wv takes the chains cbeg + wv, + nw, ..; the keys of 32 of them
@@ -1470,6 +1499,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     // pooled_big_post_kernel)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    URT_MAX(1, URT_NOW())
     __shared__ int tk;
     int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
     // acquire-release at agent scope: this block's sums are released with the
@@ -1488,9 +1518,15 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     }
   }
   if (noise_role) {
+    URT_MAX(7, ~URT_NOW())
     draw_noise(nz_worker, nz_count, nz_beg, nz_end);
+#ifdef AMH_STAMPS
+    __syncthreads();
+#endif
+    URT_MAX(6, URT_NOW())
     return;
   }
+  URT_MAX(2, URT_NOW())
   // eight waves: wave w loads / forms / writes out the columns w + 8 Q;
   // waves 0..3 factor (wave f owns the columns 16 f .. 16 f + 15)
   const int tid = threadIdx.x;
@@ -1548,6 +1584,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   US(0)
   __syncthreads();
   US(1)
+  URT_MAX(3, URT_NOW())
   // (1) the factorisation, column block f = w on waves 0..3, lane = row.
   // Every element receives column k's update for k = 0, 1, .. in order (the
   // oracle's fmaf chain), whichever wave applies it: wave f first applies
@@ -1645,6 +1682,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   }
   US(2)
   __syncthreads();
+  URT_MAX(4, URT_NOW())
   asm volatile("" ::: "memory");  // the parked values are reloaded, not kept in registers
   if (w < 4) {
     static_for<kQ8>([&](auto Q) {
@@ -1691,6 +1729,11 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   if (w == 0) p.out.loc[lane] = loc_in + gamma * (float)(sd_in / N);
   US(4)
   US_FLUSH
+#ifdef AMH_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  URT_MAX(5, URT_NOW())
 }
 
 // Sigma' = (1-g) Sigma + g S_dd / N rounded to float, in the update's

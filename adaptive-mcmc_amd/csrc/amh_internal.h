@@ -234,6 +234,7 @@ hipError_t run_chain_keys(uint32_t k0, uint32_t k1, int64_t offset, int64_t n, u
 hipError_t diag_stamps_copy(void* host, size_t bytes);
 hipError_t diag_upd_stamps_copy(void* host);
 hipError_t diag_f64_stamps_copy(void* host);
+hipError_t diag_u64_timeline_copy(void* host);
 #endif
 
 }  // namespace amh

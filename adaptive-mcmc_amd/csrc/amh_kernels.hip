@@ -1355,7 +1355,9 @@ hipError_t run_step(int model_id, const StepParams& p, hipStream_t s) {
 // ASSS at the d = 64 Gaussian (amh_asss.hip run_asss_step): the persistent
 // LDS-staged kernel around the ASSS transition
 #ifndef AMH_ASSS64_WAVES
-#define AMH_ASSS64_WAVES 12  // 170 VGPRs: the ASSS transition spilled 64 B at 16 waves (128 VGPRs)
+// 16 waves (128 VGPRs, 64 B of spill) measured 0.343 ms per sample() against
+// 0.363 ms at 12 waves (170 VGPRs, no spill): the occupancy pays for the spill
+#define AMH_ASSS64_WAVES 16
 #endif
 hipError_t run_asss_step64(const StepParams& p, hipStream_t s) {
   return launch_step64<AMH_ASSS64_WAVES, true>(p, s);
