@@ -24,13 +24,20 @@
 
 namespace amh {
 
-// memory order of the cross-block arrival tickets (acquire-release; the
-// diagnostic variant -DAMH_TICKET_RELAXED measures what the release's L2
-// write-back and the acquire's invalidate cost)
-#ifdef AMH_TICKET_RELAXED
-#define AMH_TICKET_ORDER __ATOMIC_RELAXED
-#else
+// The d = 64 update's cross-block hand-off.  The reduce blocks' sums go out
+// as agent-scope (write-through, sc1) stores and each block waits for them
+// to complete (vmcnt(0)) before its arrival ticket, so the ticket itself is a
+// relaxed RMW: an agent-scope release would add an L2 write-back
+// (buffer_wbl2) of the whole XCD, whose L2 then holds the noise blocks'
+// dirty rows -- measured 3.1 us from the last slice to the ticket, 0.7 us
+// without (tools/u64_timeline.py, r4p).  The last arriver then acquires at
+// agent scope (buffer_inv: no stale line of an earlier step's sums in its
+// L2) and reads the sums with agent-scope loads.  Diagnostic variant
+// -DAMH_TICKET_ACQREL: the acquire-release RMW instead.
+#ifdef AMH_TICKET_ACQREL
 #define AMH_TICKET_ORDER __ATOMIC_ACQ_REL
+#else
+#define AMH_TICKET_ORDER __ATOMIC_RELAXED
 #endif
 
 // fused stats kernel, drawn-ahead noise rows loaded early (diagnostic
@@ -928,22 +935,34 @@ hipError_t diag_upd_stamps_copy(void* host) {
 // each block; atomicMax of the value, or of ~value for a minimum): [0] ~first
 // block entry, [1] last reduce slice done, [2] ticket won, [3] Sigma' formed,
 // [4] factorisation done, [5] update end, [6] last noise worker end,
-// [7] ~first noise worker start.  Copied and cleared by amh_diag_u64_timeline.
-__device__ unsigned long long g_u64_rt[8];
+// [7] ~first noise worker start, [8] last reduce block's group sums in LDS,
+// [9] last reduce block's sums stored (before the vmcnt wait).  Copied and cleared by amh_diag_u64_timeline.
+__device__ unsigned long long g_u64_rt[16];
+// (kept in LDS while the block runs and flushed with atomicMax when it
+// ends, so no stamp puts a memory round trip on the path it measures)
+__shared__ unsigned long long g_urt_s[16];
+#define URT_INIT \
+  if (threadIdx.x < 16) g_urt_s[threadIdx.x] = 0ull;
 #define URT_MAX(k, v) \
-  if (threadIdx.x == 0) atomicMax(&g_u64_rt[k], (unsigned long long)(v));
+  if (threadIdx.x == 0) g_urt_s[k] = (unsigned long long)(v);
+#define URT_FLUSH \
+  if (threadIdx.x == 0)           \
+    for (int k_ = 0; k_ < 16; ++k_) \
+      if (g_urt_s[k_] != 0ull) atomicMax(&g_u64_rt[k_], g_urt_s[k_]);
 #define URT_NOW() __builtin_amdgcn_s_memrealtime()
 hipError_t diag_u64_timeline_copy(void* host) {
-  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_u64_rt), sizeof(unsigned long long) * 8, 0, hipMemcpyDeviceToHost);
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_u64_rt), sizeof(unsigned long long) * 16, 0, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return e;
-  static const unsigned long long z[8] = {0};
+  static const unsigned long long z[16] = {0};
   return hipMemcpyToSymbol(HIP_SYMBOL(g_u64_rt), z, sizeof(z), 0, hipMemcpyHostToDevice);
 }
 #else
 #define US_INIT
 #define US(k)
 #define US_FLUSH
-#define URT_MAX(k, v)
+#define URT_MAX(k, v) ;
+#define URT_INIT
+#define URT_FLUSH
 #define URT_NOW() 0ull
 #endif
 
@@ -1004,7 +1023,7 @@ __device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, i
 // (the previous column's updates) placed in the chain's dependency stalls,
 // which an in-order wave cannot fill by itself.
 template <class F>
-__device__ __forceinline__ void nr_sqrt_div(float x, float n, float& sq, float& qt, F&& fill) {
+__device__ __forceinline__ void nr_sqrt_div(float x, float n, float& sq, float& qt, float& yo, F&& fill) {
   auto step = [&](auto S) {
     __builtin_amdgcn_sched_barrier(0);
     fill(S);
@@ -1034,12 +1053,18 @@ __device__ __forceinline__ void nr_sqrt_div(float x, float n, float& sq, float& 
   step(integral_constant<int, 9>{});
   sq = x * y;
   qt = n * y;
+  yo = y;
   step(integral_constant<int, 10>{});
   step(integral_constant<int, 11>{});
   step(integral_constant<int, 12>{});
   step(integral_constant<int, 13>{});
   step(integral_constant<int, 14>{});
   step(integral_constant<int, 15>{});
+}
+template <class F>
+__device__ __forceinline__ void nr_sqrt_div(float x, float n, float& sq, float& qt, F&& fill) {
+  float y;
+  nr_sqrt_div(x, n, sq, qt, y, static_cast<F&&>(fill));
 }
 
 template <int NT>
@@ -1159,7 +1184,7 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
         static_for<32>([&](auto K) { a[K] = A[ab0 + (a4_base(d, p0 + K) - a4_base(d, p0))]; });
         US(2)
         bool ok = true;
-        float* cb = colbuf + 128 * w;  // this wave's column broadcast buffers (two, alternating)
+        float* cb = colbuf + 128 * w;  // this wave's two column broadcast rows
         // Software pipeline over the columns: column k's pivot, square root
         // and division come first; then column k-1's LDS-broadcast updates
         // (m >= k+1, read while column k was being formed) are applied; then
@@ -1167,19 +1192,37 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
         // v_readlane.  Every element still sees its updates in column order.
         f32x4 pv[8];  // column k-1's broadcast values (rows 4q .. 4q+3)
         float am1 = 0.0f;
+        // the pivot chain on wave-uniform values and the lean column of
+        // pooled_update64_kernel: next pivot = fmaf(-l1, l1, sa), l1 = n1 y;
+        // column k (unscaled) and column k + 1 to the wave's two broadcast
+        // rows at the column's start (n1, the panel rows and sa come back
+        // while the chain runs), the rows scaled by y on the way back (the
+        // vector path's q, bit for bit), column k's updates of columns k + 1
+        // and k + 2 right after it, no select for the diagonal
+        float pivu = rdlane(a[0], 0);
+        asm volatile("" : "+v"(pivu));  // a VGPR value: the seed's integer ops stay on the VALU
         static_for<32>([&](auto K) {
           constexpr int k = K;
-          const float piv = rdlane(a[k], k);
-          ok = ok && amh_pivot_ok(piv);
-          // ljj = piv y, q = a[k] y with y = amh_rsqrt_nr(piv), with column
-          // k-1's updates of the panel's columns m >= k+1 (packed pairs
-          // (m, m + 1), m even; column k + 1 alone when odd) in the chain's
-          // stalls (nr_sqrt_div; the oracle's bits)
-          float ljj, q;
-          nr_sqrt_div(piv, a[k], ljj, q, [&](auto Sl) {
+          f32x4 pn[8];
+          float sa = 0.0f;
+          if constexpr (k + 1 < 32) {
+            cb[ln] = a[k];
+            cb[64 + ln] = a[k + 1];
+            static_for<8>([&](auto Q) {
+              if constexpr (4 * Q + 3 >= k + 1) pn[(int)Q] = *(const f32x4*)&cb[4 * Q];
+            });
+            sa = cb[64 + k + 1];
+          }
+          ok = ok && amh_pivot_ok(pivu);
+          // y = amh_rsqrt_nr(piv), q = a[k] y, with column k-1's updates of
+          // the panel's columns m >= k+2 (packed pairs (m, m + 1), m even;
+          // column k + 2 alone when odd) in the chain's stalls (nr_sqrt_div;
+          // the oracle's bits)
+          float ljj, q, y;
+          nr_sqrt_div(pivu, a[k], ljj, q, y, [&](auto Sl) {
             if constexpr (k >= 1) {
-              constexpr int m0 = ((k + 1) % 2 == 0) ? k + 1 : k + 2;
-              if constexpr (Sl == 0 && m0 != k + 1) a[k + 1] = fmaf(-am1, pv[(k + 1) / 4][(k + 1) % 4], a[k + 1]);
+              constexpr int m0 = ((k + 2) % 2 == 0) ? k + 2 : k + 3;
+              if constexpr (Sl == 0 && m0 != k + 2 && k + 2 < 32) a[k + 2] = fmaf(-am1, pv[(k + 2) / 4][(k + 2) % 4], a[k + 2]);
               constexpr int m = m0 + 2 * Sl;
               if constexpr (m + 1 < 32) {
                 const f32x2v rr = __builtin_elementwise_fma(f32x2v{-am1, -am1},
@@ -1190,16 +1233,27 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
               }
             }
           });
-          a[k] = (ln == k) ? ljj : q;
+          a[k] = q;
           if constexpr (k + 1 < 32) {
-            float* cbk = cb + 64 * (k & 1);
-            cbk[ln] = a[k];
             static_for<8>([&](auto Q) {
-              if constexpr (4 * Q + 3 >= k + 2) pv[(int)Q] = *(const f32x4*)&cbk[4 * Q];
+              if constexpr (4 * Q + 3 >= k + 1) {
+                f32x4& pq = pn[(int)Q];  // whole vector live to here (pooled_update64_kernel)
+                asm volatile("" : "+v"(pq));
+              }
             });
-            am1 = a[k];
-            const float l1 = rdlane(a[k], k + 1);
-            a[k + 1] = fmaf(-a[k], l1, a[k + 1]);
+            const float n1 = pn[(k + 1) / 4][(k + 1) % 4];
+            const float l1 = n1 * y;
+            pivu = fmaf(-l1, l1, sa);
+            static_for<8>([&](auto Q) {
+              if constexpr (4 * Q + 3 >= k + 2) {  // v_pk_mul_f32 pairs
+                const f32x2v lo = f32x2v{pn[(int)Q][0], pn[(int)Q][1]} * f32x2v{y, y};
+                const f32x2v hi = f32x2v{pn[(int)Q][2], pn[(int)Q][3]} * f32x2v{y, y};
+                pv[(int)Q] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+              }
+            });
+            am1 = q;
+            a[k + 1] = fmaf(-q, l1, a[k + 1]);
+            if constexpr (k + 2 < 32) a[k + 2] = fmaf(-q, pv[(k + 2) / 4][(k + 2) % 4], a[k + 2]);
           }
           __builtin_amdgcn_sched_barrier(0);
         });
@@ -1378,9 +1432,19 @@ __device__ __forceinline__ void reduce_tiles_slice(const float* __restrict__ par
     gs[tg][c][2] = s2;
     gs[tg][c][3] = s3;
     __syncthreads();
+    if (coherent) URT_MAX(8, URT_NOW())
     if (tid < 4 * NCOL) {
-      const int64_t ng = n_groups - g0 < GT ? n_groups - g0 : GT;
-      for (int q = 0; q < ng; ++q) tot += gs[q][fc][comp];  // group order
+      const int ng = (int)(n_groups - g0 < GT ? n_groups - g0 : GT);
+      // group order; eight LDS reads in flight ahead of their adds (one read
+      // and one add at a time was a dependent LDS round trip per group)
+      for (int q0 = 0; q0 < ng; q0 += 8) {
+        double v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = gs[q0 + e < ng ? q0 + e : ng - 1][fc][comp];
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+          if (q0 + e < ng) tot += v[e];
+      }
     }
     __syncthreads();
   }
@@ -1388,6 +1452,7 @@ __device__ __forceinline__ void reduce_tiles_slice(const float* __restrict__ par
     const int64_t u = 4 * ((int64_t)blk * NCOL + fc) + comp;
     if (u < V) final_entry(u, tot, V, sums, accumulate, tile_d, fp, coherent);
   }
+  if (coherent) URT_MAX(9, URT_NOW())
 }
 
 template <int NCOL>
@@ -1417,7 +1482,8 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   __shared__ float A[d * S];
   __shared__ __attribute__((aligned(16))) float cols[64][64];  // finished factor columns (broadcast)
   __shared__ float colsum[64];
-  __shared__ int okv, done;
+  __shared__ int okv, done[64];
+  __shared__ __attribute__((aligned(16))) float bc[4][2][64];  // a factoring wave's column broadcast rows
   // the factoring waves' write-out operands, parked here while they factor
   // (they would otherwise stay live across the factorisation)
   __shared__ double park_s[kQ8][256], park_c[kQ8][256];
@@ -1439,6 +1505,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   // the noise position, read before any block can reach the update's write of
   // out.i (in place, in == out): a late reduce worker reads it in a register
   const int32_t inext = p.in.i[0] + p.K;
+  URT_INIT
   URT_MAX(0, ~URT_NOW())
   auto draw_noise = [&](int64_t worker, int64_t nworkers, int64_t cbeg, int64_t cend) {
     const int lane = lane_id();
@@ -1502,12 +1569,16 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     URT_MAX(1, URT_NOW())
     __shared__ int tk;
     int* ticket = (int*)p.scratch + d * (d + 4) / 2 + 5;
-    // acquire-release at agent scope: this block's sums are released with the
-    // ticket and the last arriver acquires every other block's
+    // a relaxed ticket after the write-through stores completed; the last
+    // arriver acquires (AMH_TICKET_ORDER above)
     if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, AMH_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
+    if (tk == nred - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last arriver: every block's sums
     if (tk != nred - 1) {  // not the last: a noise worker
-      if (nlate == 0) return;
+      if (nlate == 0) {
+        URT_FLUSH
+        return;
+      }
       noise_role = true;
       nz_worker = tk;
       nz_count = nlate;
@@ -1524,6 +1595,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     __syncthreads();
 #endif
     URT_MAX(6, URT_NOW())
+    URT_FLUSH
     return;
   }
   URT_MAX(2, URT_NOW())
@@ -1538,7 +1610,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     return coh ? __hip_atomic_load(&sums[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : sums[i];
   };
   if (tid == 0) {
-    done = 0;
+    done[0] = 0;
     okv = 1;
   }
   // (0) one batch of loads (issued before anything waits on the scalars)
@@ -1609,7 +1681,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     bool stuck = false;
     int spins = 0;
     for (int k = 0; k < c0;) {
-      int avail = __hip_atomic_load(&done, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      int avail = __hip_atomic_load(&done[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
       if (avail <= k) {
         if (++spins > (1 << 22)) {
           stuck = true;
@@ -1635,18 +1707,44 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     bool ok = true;
     f32x4 pv[4];  // column k-1's entries of this block's rows c0 .. c0 + 15
     float am1 = 0.0f;
+    // The pivot chain runs on wave-uniform values: with l1 = L_{k+1,k} =
+    // n1 y (n1 = column k's unscaled row k + 1) the next pivot is
+    // fmaf(-l1, l1, sa) (sa = row k + 1 of column k + 1 before column k's
+    // update) -- the very operations the vector update makes in lane k + 1 --
+    // so no v_readlane or LDS round trip sits between two pivots.  A lone wave
+    // is issue-bound here (tools/ubench: ~5 ticks per VALU op, dependent or
+    // not; ~15 per v_readlane feeding a VALU op; ~9 per v_cmp/v_cndmask), so
+    // the column's other work is kept small: at its start column k (unscaled)
+    // and column k + 1 go to the wave's two broadcast rows -- n1 and the
+    // rows c0 .. c0 + 15 come back from the first, sa from the second, all
+    // while the chain runs -- and the rows return scaled as pv = row y (the
+    // vector path's q, bit for bit) for the next column's fills.  Column k's
+    // updates of columns k + 1 and k + 2 are made right after it (so column
+    // k + 1 is final when its turn comes); no select for the diagonal (lane
+    // k holds the pivot itself, so its q = piv y is L_kk).
+    float pivu = rdlane(a[0], c0);
+    asm volatile("" : "+v"(pivu));  // a VGPR value: the seed's integer ops stay on the VALU
     static_for<16>([&](auto J) {
       constexpr int j = J;
       const int k = c0 + j;
-      const float piv = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[j]), k));
-      ok = ok && amh_pivot_ok(piv);
-      float ljj, q;
-      nr_sqrt_div(piv, a[j], ljj, q, [&](auto Sl) {
-        // column k-1's updates of this block's columns m >= k + 1 (packed
-        // pairs (m, m + 1), m - c0 even; column k + 1 alone when odd)
+      f32x4 pn[4];
+      float sa = 0.0f;
+      if constexpr (j + 1 < 16) {
+        bc[w][0][ln] = a[j];
+        bc[w][1][ln] = a[j + 1];
+        static_for<4>([&](auto Q) {
+          if constexpr (4 * Q + 3 >= j + 1) pn[(int)Q] = *(const f32x4*)&bc[w][0][c0 + 4 * Q];
+        });
+        sa = bc[w][1][k + 1];
+      }
+      ok = ok && amh_pivot_ok(pivu);
+      float ljj, q, y;
+      nr_sqrt_div(pivu, a[j], ljj, q, y, [&](auto Sl) {
+        // column k-1's updates of this block's columns m >= k + 2 (packed
+        // pairs (m, m + 1), m - c0 even; column k + 2 alone when odd)
         if constexpr (j >= 1) {
-          constexpr int m0 = ((j + 1) % 2 == 0) ? j + 1 : j + 2;
-          if constexpr (Sl == 0 && m0 != j + 1) a[j + 1] = fmaf(-am1, pv[(j + 1) / 4][(j + 1) % 4], a[j + 1]);
+          constexpr int m0 = ((j + 2) % 2 == 0) ? j + 2 : j + 3;
+          if constexpr (Sl == 0 && m0 != j + 2 && j + 2 < 16) a[j + 2] = fmaf(-am1, pv[(j + 2) / 4][(j + 2) % 4], a[j + 2]);
           constexpr int m = m0 + 2 * Sl;
           if constexpr (m + 1 < 16) {
             const f32x2v r = __builtin_elementwise_fma(f32x2v{-am1, -am1}, f32x2v{pv[m / 4][m % 4], pv[m / 4][m % 4 + 1]},
@@ -1656,22 +1754,41 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
           }
         }
       });
-      a[j] = (ln == k) ? ljj : q;
-      cols[k][ln] = a[j];
+      a[j] = q;
+      cols[k][ln] = q;
       if constexpr (j + 1 < 16) {
+        // the whole vectors live to here: an element never used would
+        // otherwise have its register reused while the load is in flight,
+        // and the wait for it would land inside the chain
         static_for<4>([&](auto Q) {
-          if constexpr (4 * Q + 3 >= j + 2) pv[(int)Q] = *(const f32x4*)&cols[k][c0 + 4 * Q];
+          if constexpr (4 * Q + 3 >= j + 1) {
+            f32x4& pq = pn[(int)Q];  // (a named reference: an asm operand alone is not a capture)
+            asm volatile("" : "+v"(pq));
+          }
         });
-        am1 = a[j];
-        const float l1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, a[j]), k + 1));
-        a[j + 1] = fmaf(-a[j], l1, a[j + 1]);
+        const float n1 = pn[(j + 1) / 4][(j + 1) % 4];
+        const float l1 = n1 * y;
+        pivu = fmaf(-l1, l1, sa);
+        static_for<4>([&](auto Q) {
+          if constexpr (4 * Q + 3 >= j + 2) {  // v_pk_mul_f32 pairs
+            const f32x2v lo = f32x2v{pn[(int)Q][0], pn[(int)Q][1]} * f32x2v{y, y};
+            const f32x2v hi = f32x2v{pn[(int)Q][2], pn[(int)Q][3]} * f32x2v{y, y};
+            pv[(int)Q] = f32x4{lo[0], lo[1], hi[0], hi[1]};
+          }
+        });
+        am1 = q;
+        a[j + 1] = fmaf(-q, l1, a[j + 1]);
+        if constexpr (j + 2 < 16) a[j + 2] = fmaf(-q, pv[(j + 2) / 4][(j + 2) % 4], a[j + 2]);
       }
-      // column k is out.  A wave's LDS operations are performed in issue
-      // order, so the column's writes above land before this flag; the empty
-      // asm keeps the compiler from moving them past it (a release store
-      // would also wait here for the pv reads just issued)
-      asm volatile("" ::: "memory");
-      if (ln == 0) __hip_atomic_store(&done, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      // columns out.  A wave's LDS operations are performed in issue order,
+      // so the column's writes above land before this flag; the empty asm
+      // keeps the compiler from moving them past it.  Every lane stores (lane
+      // 0 to done[0], the word the readers poll): no branch.  Every second
+      // column and the block's last.
+      if constexpr (j % 2 == 1) {
+        asm volatile("" ::: "memory");
+        __hip_atomic_store(&done[ln], k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
       __builtin_amdgcn_sched_barrier(0);
     });
     static_for<16>([&](auto J) {
@@ -1734,6 +1851,7 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   __syncthreads();
 #endif
   URT_MAX(5, URT_NOW())
+  URT_FLUSH
 }
 
 // Sigma' = (1-g) Sigma + g S_dd / N rounded to float, in the update's
@@ -1811,6 +1929,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
   }
   __syncthreads();
   if (!last) return;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the hand-off of pooled_update64_kernel)
   // as_change = sqrtf(big_sum of the column sums)
   const float v = t < d ? __uint_as_float(__hip_atomic_load(&colsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                         : 0.0f;

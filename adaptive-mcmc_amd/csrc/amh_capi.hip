@@ -843,7 +843,7 @@ int amh_diag_stamps(void* host, int64_t bytes) {
 int amh_diag_upd_stamps(void* host) { return amh::diag_upd_stamps_copy(host) == hipSuccess ? 0 : -1; }
 // pooled d = 64 fused stats kernel phase totals (16 x u64, block 0 thread 0)
 int amh_diag_f64_stamps(void* host) { return amh::diag_f64_stamps_copy(host) == hipSuccess ? 0 : -1; }
-// pooled d = 64 update launch timeline (8 x u64, 100 MHz clock; copied, then cleared)
+// pooled d = 64 update launch timeline (16 x u64, 100 MHz clock; copied, then cleared)
 int amh_diag_u64_timeline(void* host) { return amh::diag_u64_timeline_copy(host) == hipSuccess ? 0 : -1; }
 #endif
 }  // extern "C"

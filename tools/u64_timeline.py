@@ -31,7 +31,7 @@ k = PooledARWMH(potential_fn=P.correlated_gaussian(64), num_chains=a.chains, dev
 st = k.init(PRNGKey(0), 0, (torch.rand(a.chains, 64, device=dev) * 4 - 2).contiguous(), (), {})
 L = _lib.lib()
 L.amh_diag_u64_timeline.argtypes = [ctypes.c_void_p]
-buf = np.zeros(8, np.uint64)
+buf = np.zeros(16, np.uint64)
 k.sample_(st, 20)
 torch.cuda.synchronize()
 assert L.amh_diag_u64_timeline(buf.ctypes.data) == 0
@@ -44,9 +44,9 @@ for s in range(a.steps):
     rel = lambda v: (int(v) - t0) / 100.0  # noqa: E731  (10 ns ticks -> us)
     nz0 = int(~buf[7] & np.uint64(0xFFFFFFFFFFFFFFFF)) if buf[7] else None
     rows.append([rel(buf[1]), rel(buf[2]), rel(buf[3]), rel(buf[4]), rel(buf[5]), rel(buf[6]),
-                 (nz0 - t0) / 100.0 if nz0 is not None else float("nan")])
-    print("step %d: reduce done %.2f  ticket %.2f  sigma' %.2f  factor %.2f  update end %.2f  "
-          "noise %.2f..%.2f us" % (s, *rows[-1][:5], rows[-1][6], rows[-1][5]))
+                 (nz0 - t0) / 100.0 if nz0 is not None else float("nan"), rel(buf[8]), rel(buf[9])])
+    print("step %d: group sums %.2f  stored %.2f  reduce done %.2f  ticket %.2f  sigma' %.2f  factor %.2f  "
+          "update end %.2f  noise %.2f..%.2f us" % (s, rows[-1][7], rows[-1][8], *rows[-1][:5], rows[-1][6], rows[-1][5]))
 m = np.median(np.array(rows), axis=0)
-print("median: reduce done %.2f  ticket %.2f  sigma' %.2f  factor %.2f  update end %.2f  noise %.2f..%.2f us"
-      % (m[0], m[1], m[2], m[3], m[4], m[6], m[5]))
+print("median: group sums %.2f  stored %.2f  reduce done %.2f  ticket %.2f  sigma' %.2f  factor %.2f  "
+      "update end %.2f  noise %.2f..%.2f us" % (m[7], m[8], m[0], m[1], m[2], m[3], m[4], m[6], m[5]))
