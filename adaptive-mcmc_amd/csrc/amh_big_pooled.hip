@@ -32,7 +32,8 @@ namespace amh {
 // dirty rows -- measured 3.1 us from the last slice to the ticket, 0.7 us
 // without (tools/u64_timeline.py, r4p).  The last arriver then acquires at
 // agent scope (buffer_inv: no stale line of an earlier step's sums in its
-// L2) and reads the sums with agent-scope loads.  Diagnostic variant
+// L2) and reads the sums with agent-scope loads -- the write-through form of
+// cdna_hip_programming.md's in-launch counter hand-off.  Diagnostic variant
 // -DAMH_TICKET_ACQREL: the acquire-release RMW instead.
 #ifdef AMH_TICKET_ACQREL
 #define AMH_TICKET_ORDER __ATOMIC_ACQ_REL
@@ -1880,6 +1881,9 @@ __global__ __launch_bounds__(256) void pooled_big_prep_kernel(PooledUpdateParams
 // squared and summed over the column's rows r = k + t by the 256-thread
 // big_sum order (four 64-lane butterflies, (s0 + s1) + (s2 + s3)); the column
 // sums are handed to the block that finishes last, which forms as_change.
+// With pack_out (amh_pooled_step_k) the new factor also goes to the next
+// step's A-operand copy (pooled_pack_kernel's slots), so that step skips
+// its pack launch.
 __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams p) {
   const int d = p.d;
   const int k = blockIdx.x;
@@ -1911,13 +1915,21 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
       p.out.cov[o] = p.in.cov[o];
       p.out.scale[o] = lo;
     }
+    if (p.pack_out != nullptr) {  // pooled_pack_kernel's slot of L[r][k], r = k + t
+      const int r = k + t, c = k & 31;
+      const int T = r >> 5, J = k >> 5;
+      const int b = T * (T + 1) / 2 + J;
+      const int lane = (r & 31) + 32 * (c & 1);
+      p.pack_out[((int64_t)b * 256 + (c >> 3) * 64 + lane) * 4 + ((c & 7) >> 1)] = ln;
+    }
   }
   const float ws = Grp<64>::sum(sq);
   if ((t & 63) == 0) wsum[t >> 6] = ws;
   __syncthreads();
   // the column sum goes out write-through (sc1) and the block takes a ticket;
   // the block that takes the last one sums the columns (cross-XCD hand-off:
-  // sc1 stores, vmcnt(0), agent-scope add; sc1 loads by the last arriver)
+  // sc1 stores, vmcnt(0), relaxed agent-scope add, acquire + sc1 loads by the
+  // last arriver -- cdna_hip_programming.md's write-through counter recipe)
   uint32_t* colsum = (uint32_t*)(p.scratch + nA + 8);
   int* ticket = (int*)p.scratch + nA + 5;
   __shared__ int last;
@@ -1929,7 +1941,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the hand-off of pooled_update64_kernel)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   // as_change = sqrtf(big_sum of the column sums)
   const float v = t < d ? __uint_as_float(__hip_atomic_load(&colsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                         : 0.0f;
@@ -1971,10 +1983,13 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     const int nt = d / 32;
     const int64_t nch = pooled_big_chunks(p.C, d);
     float* pack = xprop;  // the caller's scratch: pooled_big_pack_floats(d) floats
-    hipLaunchKernelGGL(pooled_pack_kernel, dim3((unsigned)(nt * (nt + 1) / 2 + nt * nt)), dim3(256), 0, s, p.L,
-                       p.model.data + d, d, pack);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
+    if (!p.pack_ready) {
+      hipLaunchKernelGGL(pooled_pack_kernel, dim3((unsigned)(nt * (nt + 1) / 2 + nt * nt)), dim3(256), 0, s, p.L,
+                         p.model.data + d, d, pack);
+      e = hipGetLastError();
+      if (e != hipSuccess) return e;
+    }
     int dev = 0, cus = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);

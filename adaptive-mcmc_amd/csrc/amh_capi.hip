@@ -609,7 +609,7 @@ struct DeferredReduce {
 
 static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, int32_t k_steps,
                              float* z_out, float* pe_out, double* sums, void* stream, bool prep_for_update,
-                             bool* sigma_ready, DeferredReduce* deferred = nullptr) {
+                             bool* sigma_ready, DeferredReduce* deferred = nullptr, bool pack_ready = false) {
   if (sigma_ready) *sigma_ready = false;
   if (deferred) *deferred = DeferredReduce{};
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_stats: null handle");
@@ -657,8 +657,12 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
     // xprop + U(xprop) of the unfused path, or the fused path's A-operand copies
     const size_t nb = ((size_t)num_chains * (size_t)(d + 1) + (size_t)amh::pooled_big_pack_floats(d)) * sizeof(float);
     h->big_ready_C = -1;
+    void* const split_was = h->split_buf;
     int rc = grow(h, &h->split_buf, &h->split_bytes, nb, stream, "amh_pooled_stats/hipMalloc");
     if (rc != AMH_OK) return rc;
+    // the copies are current only when the previous update of this call wrote
+    // them into this very buffer (amh_pooled_step_k; d > 64 fused path)
+    p.pack_ready = (pack_ready && d != 64 && h->split_buf == split_was) ? 1 : 0;
     {
       // noise drawn ahead by the update launch (records checked per chain
       // by the stats kernel, so a stale or foreign buffer is never used)
@@ -713,6 +717,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
       e = amh::run_pooled_big_stats(p, h->split_buf, h->split_buf + (size_t)num_chains * d, sums,
                                     (hipStream_t)stream);
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats(MFMA path)");
+      p.pack_ready = 1;  // the K steps of a pooled block share the frozen factor
     }
     return AMH_OK;
   }
@@ -723,7 +728,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
 
 static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
                               const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready,
-                              const DeferredReduce* deferred = nullptr);
+                              const DeferredReduce* deferred = nullptr, float* pack_out = nullptr);
 
 extern "C" {
 
@@ -746,7 +751,7 @@ int amh_pooled_update_k(amh_handle* h, const double* sums, const amh_pooled_stat
 
 static int pooled_update_impl(amh_handle* h, const double* sums, const amh_pooled_state* in,
                               const amh_pooled_state* out, int32_t k_steps, void* stream, bool sigma_ready,
-                              const DeferredReduce* deferred) {
+                              const DeferredReduce* deferred, float* pack_out) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_update: null handle");
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
   if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
@@ -782,6 +787,7 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
       if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipHostMalloc");
     }
     p.err_flag = h->err_dev;
+    p.pack_out = (p.d > 64) ? pack_out : nullptr;
     if (h->noise_buf && h->noise_C > 0 && h->noise_C <= h->noise_cap && in->rng_key == h->noise_keys &&
         !noise_ahead_off()) {
       p.noise_C = h->noise_C;  // the chains (and keys) of the stats call this update follows
@@ -816,13 +822,17 @@ int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state*
   if (n_steps < 0 || sync_every < 1 || n_steps % sync_every != 0)
     return fail(h, AMH_EINVAL, "amh_pooled_step: n_steps must be a non-negative multiple of sync_every");
   const amh_pooled_state* src = in;
+  const bool big = h && h->model_id && amh::pooled_big_model(h->model_id, h->cfg.dim) && h->cfg.dim > 64;
   for (int32_t t = 0; t < n_steps; t += sync_every) {
     bool ready = false;  // one rank, no exchange: the reduction also forms Sigma'
     DeferredReduce dr;   // (d = 64: or is left to the update launch)
+    // d > 64: from the second block on, the stats launch's A-operand copy of
+    // the factor was written by the previous update's post kernel
     int rc = pooled_stats_impl(h, num_chains, src, sync_every, out->z, out->potential_energy, sums, stream, true,
-                               &ready, &dr);
+                               &ready, &dr, t > 0);
     if (rc != AMH_OK) return rc;
-    rc = pooled_update_impl(h, sums, src, out, sync_every, stream, ready, &dr);
+    rc = pooled_update_impl(h, sums, src, out, sync_every, stream, ready, &dr,
+                            (big && t + sync_every < n_steps) ? h->split_buf : nullptr);
     if (rc != AMH_OK) return rc;
     src = out;
   }

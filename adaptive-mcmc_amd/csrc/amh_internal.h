@@ -131,6 +131,9 @@ struct PooledStatsParams {
   // d = 64: the chunk partials are left for the update launch to reduce
   // (amh_pooled_step_k on one rank: the update follows with no exchange)
   int32_t defer_reduce;
+  // d > 64: the A-operand copies are current (the previous update's post
+  // kernel wrote the factor's tiles; the precision's are from the first pack)
+  int32_t pack_ready;
 };
 
 // Pool-every-K: the update after a block of K transitions that started at
@@ -164,6 +167,10 @@ struct PooledUpdateParams {
   // wait on an earlier wave's columns runs out (the factor is then kept);
   // the next library call on the handle reports it (amh_capi.hip)
   int* err_flag;
+  // d > 64, one rank (amh_pooled_step_k): pooled_big_post_kernel also writes
+  // the new factor's lower tiles in A-operand order here, for the next
+  // step's stats launch (its pooled_pack_kernel launch is then skipped)
+  float* pack_out;
 };
 int pooled_reduce64_blocks(int64_t V);  // reduce blocks of the d = 64 partial rows
 

@@ -44,6 +44,18 @@ __global__ void kern(float* out, unsigned long long* t, float s) {
       a = fmaf(a, s, c); e = fmaf(e, s, c); f = fmaf(f, s, c); g = fmaf(g, s, c);
       h = fmaf(h, s, c); k = fmaf(k, s, c); b = fmaf(b, s, c); q[0] = fmaf(q[0], s, c);
       __builtin_amdgcn_sched_barrier(0);
+    } else if constexpr (MODE == 7) {  // 8 independent v_mad_u64_u32 (4 chains x 2)
+      uint64_t* u = (uint64_t*)nullptr;
+      (void)u;
+      unsigned x0 = __float_as_uint(a), x1 = __float_as_uint(e), x2 = __float_as_uint(f), x3 = __float_as_uint(g);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const unsigned long long m0 = (unsigned long long)x0 * 0xD2511F53u, m1 = (unsigned long long)x1 * 0xCD9E8D57u;
+        const unsigned long long m2 = (unsigned long long)x2 * 0xD2511F53u, m3 = (unsigned long long)x3 * 0xCD9E8D57u;
+        x0 = (unsigned)(m0 >> 32) ^ (unsigned)m1; x1 = (unsigned)(m1 >> 32) ^ (unsigned)m2;
+        x2 = (unsigned)(m2 >> 32) ^ (unsigned)m3; x3 = (unsigned)(m3 >> 32) ^ (unsigned)m0;
+      }
+      a = __uint_as_float(x0); e = __uint_as_float(x1); f = __uint_as_float(x2); g = __uint_as_float(x3);
     } else if constexpr (MODE == 6) {  // cmp + cndmask dependent pairs
 #pragma unroll
       for (int j = 0; j < 4; ++j) { a = (li == ((i + j) & 63)) ? b : a * c; }
@@ -77,6 +89,7 @@ int main() {
     run<3>("readlane+fma (per pair)", 8, nt);
     run<4>("dep chain + 1 indep interleaved", 8, nt);
     run<6>("cmp+cndmask+mul (per triple)", 4, nt);
+    run<7>("mad_u64_u32 x8 + xor x8 (per mad)", 8, nt);
   }
   // s_memtime vs realtime calibration
   return 0;
