@@ -993,25 +993,46 @@ constexpr int kUpdWaves = AMH_UPD_WAVES;
 // A = -L_I (rows x panel columns) and B = L_J^T -- per element the fmaf chain
 // fmaf(-L_rj, L_cj, .) over j = p0 .. p0 + 31 in order, the oracle's bits.
 __device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, int I, int J, int lane) {
+  // The tile is formed transposed, D' = L_J (-L_I)^T: lane ii then holds row
+  // rI + ii of A_IJ and its registers the columns cJ + (R & 3) + 8 (R >> 2)
+  // + 4 hh, so each accumulator load / store is 32 consecutive rows of one
+  // column of the column-major A4 layout (conflict-free).  Formed as
+  // L_I (-L_J)^T instead, a register held one row of 32 different columns,
+  // 256 - 4q floats apart: a 32-way LDS bank conflict at d = 256.  The
+  // products are the same (a b = b a) in the same k order, so the bits are.
   const int hh = lane >> 5, ii = lane & 31;
   const int rI = q0 + 32 * I, cJ = q0 + 32 * J;
   f32x16 acc;
-  const int col = cJ + ii;
-  const int cb = a4_base(d, col);
-  static_for<16>([&](auto R) {
-    const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
-    acc[(int)R] = (row >= (col & ~3)) ? A[cb + row] : 0.0f;
-  });
-  static_for<16>([&](auto K2) {
-    const int k = p0 + 2 * K2 + hh;
-    const int kb = a4_base(d, k);
-    const float av = -A[kb + rI + ii];
-    const float bv = A[kb + cJ + ii];
-    acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+  const int row = rI + ii;
+  // a4_base(d, j) = gb(q) + (j & 3) s(q) with q = j >> 2, s(q) = d - 4q and
+  // gb(q) = 4 (q d - 2 q (q - 1)) - 4q: the four column groups of this lane's
+  // registers (q = cJ / 4 + 2 G + hh) once, then adds
+  int gb[4], gs[4];
+  static_for<4>([&](auto G) {
+    const int q = (cJ >> 2) + 2 * G + hh;
+    gs[G] = d - 4 * q;
+    gb[G] = 4 * (q * d - 2 * q * (q - 1)) - 4 * q + row;
   });
   static_for<16>([&](auto R) {
-    const int row = rI + (R & 3) + 8 * (R >> 2) + 4 * hh;
-    if (row >= col) A[cb + row] = acc[(int)R];
+    constexpr int G = R >> 2, c3 = R & 3;
+    const int col = cJ + c3 + 8 * G + 4 * hh;
+    acc[(int)R] = (row >= (col & ~3)) ? A[gb[G] + c3 * gs[G]] : 0.0f;
+  });
+  {
+    // k = p0 + 2 K2 + hh: group p0 / 4 + K2 / 2, k & 3 = 2 (K2 & 1) + hh
+    const int qk0 = p0 >> 2;
+    static_for<16>([&](auto K2) {
+      const int q = qk0 + (K2 >> 1);
+      const int kb = 4 * (q * d - 2 * q * (q - 1)) - 4 * q + (2 * (K2 & 1) + hh) * (d - 4 * q);
+      const float av = A[kb + cJ + ii];
+      const float bv = -A[kb + rI + ii];
+      acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
+    });
+  }
+  static_for<16>([&](auto R) {
+    constexpr int G = R >> 2, c3 = R & 3;
+    const int col = cJ + c3 + 8 * G + 4 * hh;
+    if (row >= col) A[gb[G] + c3 * gs[G]] = acc[(int)R];
   });
 }
 
@@ -1182,7 +1203,16 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
         // neighbours (never used), rows past d read row d - 1
         float a[32];
         const int ab0 = a4_base(d, p0) + r;
-        static_for<32>([&](auto K) { a[K] = A[ab0 + (a4_base(d, p0 + K) - a4_base(d, p0))]; });
+        // a4_base(d, p0 + K) - a4_base(d, p0) for K = 4 g + c (p0 = 4 q0):
+        // g (4d + 4 - 16 q0) - 8 g^2 + c (d - 4 q0 - 4 g) -- two runtime
+        // values, the rest folds (the quadratic evaluated per K was the
+        // panel's load and write-back time)
+        const int pt16 = 4 * d + 4 - 4 * p0, ps0 = d - p0;
+        auto poff = [&](auto K) {
+          constexpr int g = K >> 2, c = K & 3;
+          return g * pt16 - 8 * g * g + c * (ps0 - 4 * g);
+        };
+        static_for<32>([&](auto K) { a[K] = A[ab0 + poff(K)]; });
         US(2)
         bool ok = true;
         float* cb = colbuf + 128 * w;  // this wave's two column broadcast rows
@@ -1269,7 +1299,7 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
           // wave 0's copy of the block, none otherwise
           const int kmax = below ? (live ? 31 : -1) : (w == 0 ? ii : -1);
           static_for<32>([&](auto K) {
-            const int o = ((int)K <= kmax) ? ab0 + (a4_base(d, p0 + K) - a4_base(d, p0)) : dummy;
+            const int o = ((int)K <= kmax) ? ab0 + poff(K) : dummy;
             A[o] = a[K];
           });
         }
