@@ -1019,11 +1019,12 @@ __device__ __forceinline__ void trailing_tile(float* A, int d, int p0, int q0, i
     acc[(int)R] = (row >= (col & ~3)) ? A[gb[G] + c3 * gs[G]] : 0.0f;
   });
   {
-    // k = p0 + 2 K2 + hh: group p0 / 4 + K2 / 2, k & 3 = 2 (K2 & 1) + hh
-    const int qk0 = p0 >> 2;
+    // k = p0 + 2 K2 + hh = p0 + 4 g + c, g = K2 / 2, c = 2 (K2 & 1) + hh:
+    // a4_base(d, k) = a4_base(d, p0) + g (4d + 4 - 4 p0) - 8 g^2 + c (d - p0 - 4 g)
+    const int kb0 = a4_base(d, p0), pt16 = 4 * d + 4 - 4 * p0, ps0 = d - p0;
     static_for<16>([&](auto K2) {
-      const int q = qk0 + (K2 >> 1);
-      const int kb = 4 * (q * d - 2 * q * (q - 1)) - 4 * q + (2 * (K2 & 1) + hh) * (d - 4 * q);
+      constexpr int g = K2 >> 1, c2 = 2 * (K2 & 1);
+      const int kb = kb0 + g * pt16 - 8 * g * g + (c2 + hh) * (ps0 - 4 * g);
       const float av = A[kb + cJ + ii];
       const float bv = -A[kb + rI + ii];
       acc = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, acc, 0, 0, 0);
