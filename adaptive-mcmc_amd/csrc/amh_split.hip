@@ -299,8 +299,9 @@ __global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) 
   f32x4 a[G], y[4];
   static_for<G>([&](auto Q) { a[Q] = xa[64 * Q]; });
   static_for<4>([&](auto Q) { y[Q] = ya[Q]; });
-#pragma unroll 1
-  for (int64_t m = 0; m < NT; ++m) {
+  // one tile: KC/2 MFMA pairs, then the residues; FULL: every row exists
+  // (all tiles but the last: no per-register row test)
+  auto tile = [&](int64_t m, auto FULL) {
     f32x4 an[G], yn[4];
     const int64_t mn = (m + 1 < NT) ? m + 1 : m;  // next tile's loads in flight during this one
     static_for<G>([&](auto Q) { an[Q] = xa[(mn * G + Q) * 64]; });
@@ -317,13 +318,26 @@ __global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) 
       const float yv = y[R / 4][R % 4];
       const float e0 = (yv - (icpt0 + acc0[(int)R])) * isg0;
       const float e1 = (yv - (icpt1 + acc1[(int)R])) * isg1;
-      const bool ok = rr < nrem;
-      part0[R] = ok ? fmaf(e0, e0, part0[R]) : part0[R];
-      part1[R] = ok ? fmaf(e1, e1, part1[R]) : part1[R];
+      if constexpr (decltype(FULL)::value) {
+        part0[R] = fmaf(e0, e0, part0[R]);
+        part1[R] = fmaf(e1, e1, part1[R]);
+      } else {
+        const bool ok = rr < nrem;
+        part0[R] = ok ? fmaf(e0, e0, part0[R]) : part0[R];
+        part1[R] = ok ? fmaf(e1, e1, part1[R]) : part1[R];
+      }
     });
     static_for<G>([&](auto Q) { a[Q] = an[Q]; });
     static_for<4>([&](auto Q) { y[Q] = yn[Q]; });
-  }
+  };
+#ifdef AMH_DIA_SELECT_ALL
+#pragma unroll 1
+  for (int64_t m = 0; m < NT; ++m) tile(m, std::false_type{});
+#else
+#pragma unroll 1
+  for (int64_t m = 0; m + 1 < NT; ++m) tile(m, std::true_type{});
+  if (NT > 0) tile(NT - 1, std::false_type{});
+#endif
   // lane (i, 0) finishes chain c0, lane (i, 1) chain c1: the other half's
   // residues arrive by a 32-lane swap
   float all[32];
