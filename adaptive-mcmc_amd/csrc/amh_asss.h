@@ -55,13 +55,18 @@ __device__ __forceinline__ void asss_transition(const StepParams& p, float (&U)[
   // ---- v orthogonal to z on S^d (asss.py:219-222)
   // v - (v.z) z with one rounding per component (fmaf): with the product
   // rounded first, a draw numerically parallel to z (about 1e-9 per
-  // transition at d = 1) cancelled to exactly 0 and v / |v| was NaN
+  // transition at d = 1) cancelled to exactly 0 -- a mitigation, not a cure:
+  // if every component still rounds to 0 (|v| = 0, where the reference's
+  // v / norm(v) is NaN and would poison the chain), the transition is the
+  // shrinkage's own fallback, theta = 0 (asss.py:94): the state is kept
+  // (re-projected), the adaptation runs as usual.  Oracle: asss_chain_step.
   const float dot = Gp::sum(act ? v * zr : 0.0f) + (vd * zd);
   v = act ? fmaf(-dot, zr, v) : 0.0f;
   vd = fmaf(-dot, zd, vd);
   const float nv = sqrtf(Gp::sum(v * v) + (vd * vd));
-  v = v / nv;
-  vd = vd / nv;
+  const bool degen = !(nv > 0.0f);  // group-uniform
+  v = degen ? 0.0f : v / nv;
+  vd = degen ? 0.0f : vd / nv;
 
   // ---- S z_1d and S v_1d (asss.py:48-56 for both circle directions)
   float sz4[4] = {0.0f, 0.0f, 0.0f, 0.0f}, sv4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -101,7 +106,7 @@ __device__ __forceinline__ void asss_transition(const StepParams& p, float (&U)[
     ux = M<G>::potential(xt, r, d, mctx, lds);
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
-    cont = (pt > tpe) || (om < p.eps);
+    cont = !degen && ((pt > tpe) || (om < p.eps));
   }
   while (__ballot(cont) != 0ull) {
     const float thmin_n = (th < 0.0f) ? th : thmin;
@@ -124,7 +129,7 @@ __device__ __forceinline__ void asss_transition(const StepParams& p, float (&U)[
       cont = (iter < kAsssMaxIter) && ((pt > tpe) || (om < p.eps));
     }
   }
-  const bool capped = iter >= kAsssMaxIter;  // asss.py:94: theta = 0
+  const bool capped = degen || iter >= kAsssMaxIter;  // asss.py:94: theta = 0
   const float xnew = capped ? x0 : xt;
   float pen = capped ? U0 : ux;
   if (amh_isnan(pen)) pen = INFINITY;  // asss.py:234

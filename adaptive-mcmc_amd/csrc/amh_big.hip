@@ -179,14 +179,13 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
     const float el = amh_expf(p.in.log_step_size[c]);
     float inv[kNS], xi[kNS], eta[kNS], zz[kNS], mu[kNS], acc[kNS], sa[kNS], sr[kNS], zp[kNS], wa[kNS], wr[kNS];
     float pdl[kNS];
+    step_noise_rows<kNS>(lane, d, (uint32_t)it, k0, k1, xi);  // bit spec: amh_step_word
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       const float dl = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
       pdl[K] = dl;
       inv[K] = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-      xi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
       eta[K] = dl * xi[K];
       zz[K] = act ? p.in.z[c * d + r] : 0.0f;
       mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
@@ -255,7 +254,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     const float macc = p.in.mean_accept_prob[c];
     const float lam = p.in.log_step_size[c];
     float pep = p.pep[c];
-    const float u = amh_unif01_from_bits(amh_philox4x32_10(0u, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1).v[1]);
+    const float u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)it, k0, k1));  // W_d
     if (amh_isnan(pep)) pep = INFINITY;
     const float ex = amh_expf(pe - pep);
     const float alpha = (ex > 1.0f) ? 1.0f : ex;
@@ -313,14 +312,13 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     // next transition's propose state (big_propose_kernel on the output state)
     float ninv[kNS], nxi[kNS], neta[kNS], nacc[kNS], nsa[kNS], nsr[kNS], nzp[kNS], nwa[kNS], nwr[kNS], ndg[kNS];
     if constexpr (NEXT) {
+      step_noise_rows<kNS>(lane, d, (uint32_t)itr, k0, k1, nxi);
       static_for<kNS>([&](auto K) {
         const int r = 64 * K + lane;
         const bool act = r < d;
         const float ndl = act ? (revert ? dl[K] : 1.0f * qq[K]) : 0.0f;
         ndg[K] = ndl;
         ninv[K] = (amh_isfinite(ndl) && ndl != 0.0f) ? 1.0f / ndl : 0.0f;
-        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)itr, 0u, AMH_TAG_STEP, k0, k1);
-        nxi[K] = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
         neta[K] = ndl * nxi[K];
         nacc[K] = nsa[K] = nsr[K] = nzp[K] = nwa[K] = nwr[K] = 0.0f;
       });

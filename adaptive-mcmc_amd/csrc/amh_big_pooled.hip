@@ -207,23 +207,27 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   // previous update launch when the chain's record is this draw's (i, key),
   // else here.  PRE: the rows are already in xr0 (sub-chunk 0: the prologue)
   float xr0[16];
-  auto noise_phase = [&](int64_t c0, auto PRE) {
+  auto noise_phase = [&](int64_t c0, auto PRE, int32_t its, uint32_t krv, bool records) {
     uint64_t usem = 0;
-    if (ahead) {
-      // lane N < 16: key word 0 of chain N is its own kr, word 1 lane N + 16's
-      const uint32_t kw1 = (uint32_t)__shfl_down((int)kr, 16, 64);
-      const bool ok = (lane < 16) && rec.x == (uint32_t)it && rec.y == kr && rec.z == kw1;
+    if (ahead && records) {
+      // lane N < 16: key word 0 of chain N is its own krv, word 1 lane N + 16's
+      const uint32_t kw1 = (uint32_t)__shfl_down((int)krv, 16, 64);
+      const bool ok = (lane < 16) && rec.x == (uint32_t)its && rec.y == krv && rec.z == kw1;
       usem = __ballot(ok);
     }
     if (usem == 0xFFFFull) {  // every chain of the wave: rows of the buffer (one latency)
       float xr[16];
+      // the rows through one buffer descriptor with a wave-uniform base (rows
+      // past C read 0 -- unused): 64-bit per-lane addresses here were hoisted
+      // out of the step loop and spilled, 16 of them
+      const int64_t cw = c0 + w;
+      const int64_t nrow = p.C - cw;
+      const Buf xb(uniform_ptr(p.xi + cw * d), (uint32_t)((nrow > 0 ? nrow : 0) * d) * 4u);
       static_for<16>([&](auto N) {
         if constexpr (decltype(PRE)::value) {
           xr[N] = xr0[N];
         } else {
-          int64_t ch = c0 + w + 4 * N;
-          if (ch >= p.C) ch = p.C - 1;
-          xr[N] = p.xi[ch * d + lane];
+          xr[N] = xb.ld(4u * (uint32_t)lane, 4u * (uint32_t)(4 * (int)N * d));
         }
       });
       static_for<16>([&](auto N) {
@@ -233,22 +237,32 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
         if (lane == 0) uu[cc] = amh_unif01_from_bits(ub);
       });
     } else {
-      static_for<16>([&](auto N) {
-        const int cc = w + 4 * N;
-        if ((usem >> N) & 1) {
-          int64_t ch = c0 + cc;
-          Xi[cc * kFS + fperm(lane)] = p.xi[ch * d + lane];
-          const uint32_t ub = (uint32_t)__builtin_amdgcn_readlane((int)rec.w, N);
-          if (lane == 0) uu[cc] = amh_unif01_from_bits(ub);
-        } else {
-          const uint32_t k0 = (uint32_t)__builtin_amdgcn_readlane((int)kr, N);
-          const uint32_t k1 = (uint32_t)__builtin_amdgcn_readlane((int)kr, 16 + N);
-          const amh_u32x4 o = amh_philox4x32_10((uint32_t)lane, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-          Xi[cc * kFS + fperm(lane)] = amh_normal_from_bits(o.v[0]);
-          if (lane == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
-        }
-        __builtin_amdgcn_sched_barrier(0);  // one chain at a time (the rare path: keeps registers for the rest)
+      // not every chain's row was drawn ahead: the wave draws all 16 here (the
+      // buffer holds the same values).  Bit spec (amh_step_word): pass g
+      // draws chains w + 4 (4 g + (lane >> 4)), call c = lane & 15 = the
+      // coordinates 4c .. 4c + 3; one more pass the uniforms (call 16, word
+      // 0).  Five Philox calls per lane for 16 chains (one per normal: 16).
+      // (an opaque copy of the lane id: the shuffle addresses are formed here,
+      // not hoisted out of the step loop -- they spilled)
+      int ln = lane;
+      asm volatile("" : "+v"(ln));
+      const int cq = ln & 15;
+      static_for<4>([&](auto G4) {
+        const int N = 4 * G4 + (ln >> 4);
+        const uint32_t k0 = (uint32_t)__shfl((int)krv, N, 64), k1 = (uint32_t)__shfl((int)krv, 16 + N, 64);
+        const amh_u32x4 o = amh_philox4x32_10((uint32_t)cq, (uint32_t)its, 0u, AMH_TAG_STEP, k0, k1);
+        float* row = Xi + (w + 4 * N) * kFS;
+        static_for<4>([&](auto E) {
+          row[fperm(4 * cq + E)] = amh_normal_from_bits(o.v[E]);
+          __builtin_amdgcn_sched_barrier(0);  // one normal at a time (registers for the rest of the kernel)
+        });
       });
+      {
+        const int N = ln & 15;
+        const uint32_t k0 = (uint32_t)__shfl((int)krv, N, 64), k1 = (uint32_t)__shfl((int)krv, 16 + N, 64);
+        const amh_u32x4 o = amh_philox4x32_10(16u, (uint32_t)its, 0u, AMH_TAG_STEP, k0, k1);
+        if (ln < 16) uu[w + 4 * ln] = amh_unif01_from_bits(o.v[0]);
+      }
     }
   };
   // the first sub-chunk's loads -- z, keys, records, pe and (speculatively)
@@ -289,21 +303,40 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   }
   if (nmine > 0) {
     store_z();
-    if constexpr (kF64Pre0) noise_phase(sub_c0(0), std::true_type{});  // sub-chunk 0's phase (1), its rows already loaded
-    else noise_phase(sub_c0(0), std::false_type{});
+    if constexpr (kF64Pre0) noise_phase(sub_c0(0), std::true_type{}, it, kr, true);  // sub-chunk 0's phase (1), its rows already loaded
+    else noise_phase(sub_c0(0), std::false_type{}, it, kr, true);
   }
   lds_barrier();
   FS(14)
   bool pre_ok = false;  // this sub-chunk's noise rows were written during the previous one
+  // A pooled block of K steps (sync_every = K) runs in this one launch: a
+  // sub-chunk's chains take their K transitions back to back (z in LDS, pe
+  // in wave 0's registers between them) before the next sub-chunk, and the
+  // chunk's sums run over (sub-chunk, step, chain) -- orc_pooled_stats64_k.
+  // Step 0's noise may come from the buffer the update launch drew ahead;
+  // the others are drawn here (noise_phase).
+  const int32_t K = p.k_steps;
+  int64_t q = 0;  // steps of this block so far (tile parity)
   for (int64_t t = 0; t < nmine; ++t) {
     const int64_t c0 = sub_c0(t);
     const int64_t left = p.C - c0;
     const int nv = left < kFSub ? (int)left : kFSub;
-    Xi = (t & 1) ? XB : XA;
-    Xp = (t & 1) ? XA : XB;
-    if (t > 0 && !pre_ok) noise_phase(c0, std::false_type{});
     const bool more = t + 1 < nmine;
-    if (more) load_sub(t + 1);  // in flight through phases (2) .. (6)
+#pragma unroll 1
+   for (int32_t s = 0; s < K; ++s, ++q) {
+    const bool fin = s == K - 1;  // the sub-chunk's last step: z, pe go out, the next sub-chunk comes in
+    // per-lane LDS / memory offsets from an opaque copy of the lane id, formed
+    // in each step: hoisted out of the step loop they exceeded the registers
+    // (two waves per SIMD) and spilled
+    int lane_o = lane_id();
+    asm volatile("" : "+v"(lane_o));
+    const int lane = lane_o;
+    const int h = lane >> 5, i = lane & 31;
+    Xi = (q & 1) ? XB : XA;
+    Xp = (q & 1) ? XA : XB;
+    // (records are for step 0: the update launch draws the next block's first step)
+    if ((t > 0 || s > 0) && !pre_ok) noise_phase(c0, std::false_type{}, it + s, kr, s == 0);
+    if (fin && more) load_sub(t + 1);  // in flight through phases (2) .. (6) of the last step
     FS(0)
     lds_barrier();
     FS(1)
@@ -366,11 +399,12 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
         const float ex = amh_expf(pev - pp);
         a = (ex > 1.0f) ? 1.0f : ex;
         acc_f = uu[lane] < a;
-        p.pe_out[c0 + lane] = acc_f ? pp : pev;
+        pev = acc_f ? pp : pev;
+        if (fin) p.pe_out[c0 + lane] = pev;
       }
       flag[lane] = acc_f;
       alph[lane] = a;
-      if (more) load_pe(t + 1);
+      if (fin && more) load_pe(t + 1);
     }
     FS(6)
     lds_barrier();
@@ -379,7 +413,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     // load_sub(t + 1) in phase (1)) and written to its tile in phase (6)
     float xn[16];
     bool pre_next = false;
-    if (kF64Pre && more && ahead) {
+    if (kF64Pre && K == 1 && more && ahead) {
       const int64_t c1 = sub_c0(t + 1);
       static_for<16>([&](auto N) {
         int64_t ch = c1 + w + 4 * N;
@@ -403,9 +437,10 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
         const int cc = w + 4 * N;
         float dv = 0.0f;
         if (cc < nv) {
-          p.z_out[(c0 + cc) * d + lane] = zn[N];
+          if (fin) p.z_out[(c0 + cc) * d + lane] = zn[N];
           dv = zn[N] - mu_l;
         }
+        if (!fin) Zs[cc * kFS + lane] = zn[N];  // the next step's z (this lane read the slot above)
         Xi[lane * kFS + fperm(cc)] = dv;
       });
     }
@@ -423,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     pre_ok = pre_next;
     // ---- (6) the chunk's sums, accumulated over its sub-chunks in chain order
     {
-      const bool last = (t % kSub == kSub - 1) || !more;  // the chunk's last sub-chunk
+      const bool last = fin && ((t % kSub == kSub - 1) || !more);  // the chunk's last sub-chunk, last step
       float* out = (float*)p.partials + (c0 / kFChunk) * Vt;
       if (w < 3) {
         const int pI = (w == 0) ? 0 : 1, pJ = (w == 2) ? 1 : 0;
@@ -475,10 +510,11 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
         }
       }
     }
-    if (more) store_z();  // every wave is past its phase-(5) reads of z
+    if (fin && more) store_z();  // every wave is past its phase-(5) reads of z
     FS(10)
     lds_barrier();
     FS(11)
+   }
   }
   FS_FLUSH
 }
@@ -650,13 +686,17 @@ __global__ __launch_bounds__(512) void pooled_fused_big_kernel(PooledStatsParams
             });
           } else {
           const uint32_t kk0 = p.keys[2 * ch], kk1 = p.keys[2 * ch + 1];
+#ifndef AMH_FB_NORNG
+          float xr[NQ];
+          uint32_t ubw;
+          step_noise_rows<NQ>(lane, D, (uint32_t)it, kk0, kk1, xr, &ubw);  // bit spec: amh_step_word
+#endif
           static_for<NQ>([&](auto Q) {
             const int k = 64 * Q + lane;
             if (k < D) {
 #ifndef AMH_FB_NORNG
-              const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)it, 0u, AMH_TAG_STEP, kk0, kk1);
-              Xb[k * kLd + cc] = amh_normal_from_bits(o.v[0]);
-              if (k == 0) uu[cc] = amh_unif01_from_bits(o.v[1]);
+              Xb[k * kLd + cc] = xr[Q];
+              if (k == 0) uu[cc] = amh_unif01_from_bits(ubw);
 #else
               Xb[k * kLd + cc] = (float)((kk0 + k) & 15) * 0.1f - 0.75f;
               if (k == 0) uu[cc] = 0.5f;
@@ -1096,9 +1136,9 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
   constexpr int d = 32 * NT;  // compile-time: the A4 offsets of every phase fold to constants
   if (blockIdx.x > 0) {
     // extra blocks (one per CU, beside the single-workgroup factorisation):
-    // the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
-    // Philox(0, i', 0)[1] of every chain, i' = i + K (pooled_big_prep_kernel
-    // left it in the staging buffer), each chain's row with its record
+    // the next step's noise xi and u bits of every chain at i' = i + K
+    // (the step stream, amh_step_word; pooled_big_prep_kernel left i' in the
+    // staging buffer), each chain's row with its record
     const int32_t inext = ((const int*)p.scratch)[d * (d + 4) / 2 + 4];
     const int lane = lane_id();
     const int64_t wv = (int64_t)(blockIdx.x - 1) * kUpdWaves + threadIdx.x / 64;
@@ -1106,13 +1146,11 @@ __global__ __launch_bounds__(64 * kUpdWaves) void pooled_big_update_kernel(Poole
     for (int64_t ch = wv; ch < p.noise_C; ch += nw) {
       const uint32_t kk0 = p.keys[2 * ch], kk1 = p.keys[2 * ch + 1];
       uint32_t ubits = 0u;
+      float xr[(d + 63) / 64];
+      step_noise_rows<(d + 63) / 64>(lane, d, (uint32_t)inext, kk0, kk1, xr, &ubits);  // bit spec: amh_step_word
       static_for<(d + 63) / 64>([&](auto Q) {
         const int k = 64 * Q + lane;
-        if (k < d) {
-          const amh_u32x4 o = amh_philox4x32_10((uint32_t)k, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0, kk1);
-          p.xi[ch * d + k] = amh_normal_from_bits(o.v[0]);
-          if (k == 0) ubits = o.v[1];
-        }
+        if (k < d) p.xi[ch * d + k] = xr[Q];
       });
       if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0, kk1, ubits);
     }
@@ -1522,8 +1560,8 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   __shared__ float park_l[kQ8][256];
   const int nred = p.red_blocks;        // > 0: reduce the chunk partials first
   const int base = nred > 0 ? nred : 1;  // blocks [0, base): reduce / update; the rest draw noise
-  // the next step's noise xi_k = N(Philox(k, i', 0)[0]) and u bits
-  // Philox(0, i', 0)[1] of every chain, i' = i + K, each chain's row with its
+  // the next step's noise xi and u bits of every chain at i' = i + K (the
+  // step stream, amh_step_word), each chain's row with its
   // record (the stats kernel uses a row only if the record is its draw), by
   // `nworkers` 8-wave workers: the noise blocks, and the reduce blocks that
   // do not run the update (after their slice) -- every CU but the update's
@@ -1541,46 +1579,43 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
   URT_MAX(0, ~URT_NOW())
   auto draw_noise = [&](int64_t worker, int64_t nworkers, int64_t cbeg, int64_t cend) {
     const int lane = lane_id();
-    // wave wv takes the chains cbeg + wv, + nw, ..; the keys of 32 of them
-    // arrive in one vector load (lane l: word l & 1 of the (l >> 1)-th)
+    // wave wv takes the chains cbeg + wv, + nw, .. in batches of 64 (lane l
+    // loads the key of the batch's l-th).  Bit spec (amh_step_word): per
+    // chain the 16 calls 0..15 give the 64 normals (word k of call c is
+    // coordinate 4c + k) and call 16's word 0 the accept uniform.  One pass
+    // draws four chains (lane >> 4) x 16 calls (lane & 15) -- four normals
+    // per lane, stored as one 16-B vector (each chain's 256-B row
+    // contiguous) -- and one more pass per batch the 64 uniforms with the
+    // records: 17 Philox calls per 64 chains per lane where one call per
+    // normal took 64.
     const int64_t wv = cbeg + worker * 8 + threadIdx.x / 64;
     const int64_t nw = nworkers * 8;
-    // Four chains per group, straight-line (unrolled rounds, no branch:
-    // a chain past noise_C repeats the last one and does not store), so the
-    // four independent Philox / erfinv chains interleave -- one chain at a
-    // time left the wave waiting on each dependent 64-bit multiply.
-    for (int64_t c32 = wv; c32 < cend; c32 += 32 * nw) {
-      int64_t kc = c32 + nw * (lane >> 1);
-      if (kc >= cend) kc = cend - 1;
-      const uint32_t kv = p.keys[2 * kc + (lane & 1)];
-      static_for<8>([&](auto G) {
-        if (c32 + nw * (4 * G) >= cend) return;  // (wave-uniform) no chain of this group left
+    for (int64_t c64 = wv; c64 < cend; c64 += 64 * nw) {
+      const int64_t mc = c64 + nw * lane;
+      const int64_t mcl = mc < cend ? mc : cend - 1;
+      const uint32_t mk0 = p.keys[2 * mcl], mk1 = p.keys[2 * mcl + 1];
+      {
+        const amh_u32x4 o = amh_philox4x32_10(16u, (uint32_t)inext, 0u, AMH_TAG_STEP, mk0, mk1);
+        if (mc < cend) p.xrec[mc] = make_uint4((uint32_t)inext, mk0, mk1, o.v[0]);
+      }
+      const int cq = lane & 15;
+      for (int g = 0; g < 16; ++g) {
+        if (c64 + nw * (4 * g) >= cend) break;  // (wave-uniform) no chain of this pass left
+        const int j = 4 * g + (lane >> 4);
+        const uint32_t k0 = (uint32_t)__shfl((int)mk0, j, 64), k1 = (uint32_t)__shfl((int)mk1, j, 64);
+        const amh_u32x4 o = amh_philox4x32_10_unrolled((uint32_t)cq, (uint32_t)inext, 0u, AMH_TAG_STEP, k0, k1);
         float xv[4], uv[4], wv0[4];
-        uint32_t kk0[4], kk1[4], ub[4];
-        static_for<4>([&](auto E) {  // amh_normal_from_bits, the tail only where a lane needs it
-          constexpr int J = 4 * G + E;
-          kk0[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J);
-          kk1[E] = (uint32_t)__builtin_amdgcn_readlane((int)kv, 2 * J + 1);
-          const amh_u32x4 o = amh_philox4x32_10_unrolled((uint32_t)lane, (uint32_t)inext, 0u, AMH_TAG_STEP, kk0[E], kk1[E]);
-          xv[E] = amh_normal_head(o.v[0], &uv[E], &wv0[E]);
-          ub[E] = (uint32_t)__builtin_amdgcn_readlane((int)o.v[1], 0);
-        });
-        static_for<4>([&](auto E) {
+        static_for<4>([&](auto E) { xv[E] = amh_normal_head(o.v[E], &uv[E], &wv0[E]); });
+        static_for<4>([&](auto E) {  // the erfinv tail only where some lane needs it
           if (__builtin_amdgcn_ballot_w64(!(wv0[E] < 5.0f)) != 0) {
             const float pl = amh_erfinv_tail(wv0[E]);
             xv[E] = (wv0[E] < 5.0f) ? xv[E] : pl;
           }
           xv[E] = 1.41421356f * (xv[E] * uv[E]);
         });
-        static_for<4>([&](auto E) {
-          const int64_t ch = c32 + nw * (4 * G + E);
-          if (ch < cend) {
-            p.xi[ch * d + lane] = xv[E];
-            if (lane == 0) p.xrec[ch] = make_uint4((uint32_t)inext, kk0[E], kk1[E], ub[E]);
-          }
-        });
-        __builtin_amdgcn_sched_barrier(0);
-      });
+        const int64_t ch = c64 + nw * j;
+        if (ch < cend) *(f32x4*)(p.xi + ch * d + 4 * cq) = f32x4{xv[0], xv[1], xv[2], xv[3]};
+      }
     }
   };
   // one call site of draw_noise (two inlined copies cost the update path

@@ -173,9 +173,17 @@ int amh_create(const amh_config* cfg, int device, amh_handle** out) {
   return AMH_OK;
 }
 
+int amh_check_device(amh_handle* h) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_check_device: null handle");
+  return check_device_flag(h);
+}
+
 int amh_destroy(amh_handle* h) {
+  int rc = AMH_OK;
   if (h) {
     (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();  // the handle's last launches may still write its flag
+    if (h->err_host && *(volatile int*)h->err_host != 0) rc = fail(nullptr, AMH_EHIP, kUpdateStuck);
     if (h->gamma_tab) (void)hipFree(h->gamma_tab);
     if (h->partials) (void)hipFree(h->partials);
     if (h->split_buf) (void)hipFree(h->split_buf);
@@ -185,7 +193,7 @@ int amh_destroy(amh_handle* h) {
     if (h->err_host) (void)hipHostFree(h->err_host);
   }
   delete h;
-  return AMH_OK;
+  return rc;
 }
 
 int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n_data, const int64_t* iparams,
@@ -690,10 +698,13 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
         }
       }
     }
-    // one launch sequence per step of the block, the sums accumulated
-    for (int32_t t = 0; t < k_steps; ++t) {
-      p.i_add = t;
-      p.accumulate = t > 0;
+    // one launch sequence per step of the block, the sums accumulated; d = 64:
+    // the block's K steps in one launch (pooled_fused64_kernel, p.k_steps)
+    const int32_t n_launch = (d == 64) ? 1 : k_steps;
+    for (int32_t t0 = 0; t0 < n_launch; ++t0) {
+      const int32_t t = (d == 64) ? k_steps - 1 : t0;  // the step the launch ends with
+      p.i_add = (d == 64) ? 0 : t;
+      p.accumulate = (d == 64) ? 0 : t > 0;
       if (prep_for_update && d != 64 && t == k_steps - 1) {
         p.prep.cov = in->cov;
         p.prep.i = in->i;
@@ -704,7 +715,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
         p.prep.a = h->cfg.lr_decay;
         if (sigma_ready) *sigma_ready = true;
       }
-      if (t > 0) {
+      if (t0 > 0) {
         p.z = z_out;
         p.pe = pe_out;
       }

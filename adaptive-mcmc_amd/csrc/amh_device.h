@@ -146,6 +146,66 @@ struct Grp {
   }
 };
 
+// ------------------------------------------------------ the step's noise --
+// Bit spec (include/amh_math.h amh_step_word): words W_j = Philox(j >> 2, it,
+// 0, TAG_STEP; key)[j & 3]; xi_r = N(W_r) for r < d, u = U(W_d).  In a
+// chain's G-lane group (G >= d) lane r computes call r >> 2 itself (four
+// lanes the same call: no cross-lane traffic, one call per lane as before)
+// and keeps word r & 3.  u is word d & 3 of call d >> 2, which lane
+// 4 (d >> 2) computed when that lane is in the group (d < G, or d % 4 != 0);
+// else (d = G, a multiple of 4) one more call.
+template <int G>
+__device__ __forceinline__ void step_noise(int r, int d, uint32_t it, uint32_t k0, uint32_t k1, float& xi, float& u) {
+  const amh_u32x4 o = amh_philox4x32_10((uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
+  const int q = r & 3;
+  const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
+  xi = amh_normal_from_bits(w);
+  const int qd = d & 3;
+  const int src = 4 * (d >> 2);
+  uint32_t ub;
+  if (src < G) {
+    const uint32_t us = (qd == 0) ? o.v[0] : ((qd == 1) ? o.v[1] : ((qd == 2) ? o.v[2] : o.v[3]));
+    ub = (uint32_t)__float_as_int(Grp<G>::bcast_rt(__int_as_float((int)us), src));
+  } else {
+    ub = amh_philox4x32_10((uint32_t)(d >> 2), it, 0u, AMH_TAG_STEP, k0, k1).v[0];
+  }
+  u = amh_unif01_from_bits(ub);
+}
+
+// One chain per wave at d = 64 (arwmh_step64_kernel): lane r computes call
+// r >> 2 itself (four lanes the same call -- no cross-lane traffic, and the
+// registers of the bpermute form, which made the kernel spill) and keeps word
+// r & 3; u's call 16 runs on the scalar unit (the key and position are
+// wave-uniform).  The same bits as step_noise<64>.
+__device__ __forceinline__ void step_noise_w64(int r, uint32_t it, uint32_t k0, uint32_t k1, float& xi, float& u) {
+  const amh_u32x4 o = amh_philox4x32_10((uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
+  const int q = r & 3;
+  const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
+  xi = amh_normal_from_bits(w);
+  const uint32_t ks0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k0);
+  const uint32_t ks1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
+  const uint32_t its = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
+  u = amh_unif01_from_bits(amh_philox4x32_10(16u, its, 0u, AMH_TAG_STEP, ks0, ks1).v[0]);
+}
+
+// The same stream for one chain per wave with lane l owning rows 64 K + l
+// (the large-d kernels, NS row slices): row 64 K + l is word l & 3 of call
+// 16 K + (l >> 2), computed by the lane itself (NS calls per lane, as one per
+// row was; no cross-lane traffic).  Rows >= d get 0.  *ubits (if given)
+// receives word d, the accept uniform's bits (one more call).
+template <int NS>
+__device__ __forceinline__ void step_noise_rows(int lane, int d, uint32_t it, uint32_t k0, uint32_t k1,
+                                                float (&xi)[NS], uint32_t* ubits = nullptr) {
+  static_assert(NS <= 4, "64 calls cover 256 rows");
+  const int q = lane & 3;
+  static_for<NS>([&](auto K) {
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)(16 * (int)K + (lane >> 2)), it, 0u, AMH_TAG_STEP, k0, k1);
+    const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
+    xi[K] = (64 * (int)K + lane < d) ? amh_normal_from_bits(w) : 0.0f;
+  });
+  if (ubits != nullptr) *ubits = amh_step_word((uint32_t)d, it, k0, k1);
+}
+
 // ----------------------------------------------------------- lane masks --
 // Per-column lane predicates of the load/store phases.  For a full-wave
 // group they are compile-time lane masks built by one SALU shift inside the

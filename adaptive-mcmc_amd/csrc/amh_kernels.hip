@@ -364,9 +364,9 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
-      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      float xi, u;
+      step_noise<G>(r, d, (uint32_t)it, k0, k1, xi, u);
+      xi = act ? xi : 0.0f;
 
       // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
       //      L xi = U (dl * xi)
@@ -513,8 +513,9 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       if (p.xprop_next != nullptr) {
         const bool any_upd = Gp::any(updated);
         const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
-        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-        const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+        float xi, u_unused;
+        step_noise<G>(r, d, (uint32_t)it, k0, k1, xi, u_unused);
+        xi = act ? xi : 0.0f;
         const float el = amh_expf(lam);
         const float eta = dl * xi;
         float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
@@ -675,9 +676,9 @@ __global__ __launch_bounds__(kBlock) void sample_pnx_kernel(PnxParams p) {
     float z = act ? p.x[pt * d + r] : 0.0f;
     float pe = M<G>::potential(z, r, d, mctx, lds);
     for (int32_t t = 0; t < p.n; ++t) {
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)t, 0u, AMH_TAG_STEP, kk.v[0], kk.v[1]);
-      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
-      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      float xi, u;
+      step_noise<G>(r, d, (uint32_t)t, kk.v[0], kk.v[1], xi, u);
+      xi = act ? xi : 0.0f;
       float acc = 0.0f;
       static_for<DMAX>([&](auto J) {
         if (J < d) acc = fmaf(A[J], Gp::template bcast<J>(xi), acc);
@@ -1000,9 +1001,8 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       it += 1;
      } else {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-      const float xi = amh_normal_from_bits(o.v[0]);
-      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      float xi, u;
+      step_noise_w64(r, (uint32_t)it, k0, k1, xi, u);  // bit spec: amh_step_word
 
       // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167), L xi = U (dl * xi)
       const float el = amh_expf(lam);

@@ -132,9 +132,9 @@ __global__ __launch_bounds__(kPoolWaves * 64) void pooled_stats_kernel(PooledSta
     // K transitions with the frozen shared state (K = 1: one pooled step)
     for (int t = 0; t < K; ++t) {
       // noise at the shared stream position i + t (arwmh.py:162-165, 174)
-      const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)(it + t), 0u, AMH_TAG_STEP, k0, k1);
-      const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
-      const float u = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[1]));
+      float xi, u;
+      step_noise<G>(r, d, (uint32_t)(it + t), k0, k1, xi, u);
+      xi = act ? xi : 0.0f;
       // proposal with the shared factor (arwmh.py:166-167)
       const float acc = lds_row_dot64(prow, d, xi, act);
       const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;

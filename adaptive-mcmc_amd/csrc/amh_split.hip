@@ -78,8 +78,9 @@ __global__ __launch_bounds__(kBlock) void propose_kernel(StepParams p, float* __
         U[j] = (r == j) ? 1.0f : ((r > j) ? U[j] * ij : 0.0f);
       }
     });
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-    const float xi = act ? amh_normal_from_bits(o.v[0]) : 0.0f;
+    float xi, u_unused;
+    step_noise<G>(r, d, (uint32_t)it, k0, k1, xi, u_unused);  // (bit spec: amh_step_word)
+    xi = act ? xi : 0.0f;
     const float el = amh_expf(lam);
     const float eta = dl * xi;
     float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};

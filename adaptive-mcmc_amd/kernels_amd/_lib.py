@@ -31,7 +31,7 @@ EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bi
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
-           "amh_normals", "amh_sinkhorn_lse")
+           "amh_normals", "amh_sinkhorn_lse", "amh_check_device")
 
 
 class AmhConfig(ctypes.Structure):
@@ -81,6 +81,8 @@ def lib():
     L.amh_last_error.restype = ctypes.c_char_p
     L.amh_create.argtypes = [ctypes.POINTER(AmhConfig), ctypes.c_int, ctypes.POINTER(P)]
     L.amh_destroy.argtypes = [P]
+    L.amh_check_device.argtypes = [P]
+    L.amh_check_device.restype = ctypes.c_int
     L.amh_bind_model.argtypes = [P, I32, P, I64, ctypes.POINTER(I64), I32]
     L.amh_init.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), I64, I64, P, ctypes.POINTER(AmhState), P]
     L.amh_step.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), I32,
@@ -175,8 +177,12 @@ class Handle:
 
     def close(self):
         if getattr(self, "h", None) is not None and self.h.value:
-            self._lib.amh_destroy(self.h)
+            rc = self._lib.amh_destroy(self.h)
             self.h = None
+            if rc != 0:  # a device-side failure nobody had collected (amh_check_device)
+                import warnings
+                msg = self._lib.amh_last_error(None)
+                warnings.warn(f"libamh: {msg.decode() if msg else rc}", RuntimeWarning)
 
     def __del__(self):
         try:

@@ -92,6 +92,10 @@ class PooledARWMH(ARWMH):
         # all-reduce on the side stream, update launch) even in a world of one
         # rank, so the RCCL branch can be exercised and timed on one GPU
         self.force_collective = False
+        # A/B: the non-overlapped all-reduce through torch.distributed on its
+        # side stream (the round-4 path) instead of RCCL on the compute stream
+        self.torch_stream_collective = False
+        self._rccl_comm = None
 
     def _world(self) -> int:
         if not dist.is_available() or not dist.is_initialized():
@@ -151,14 +155,23 @@ class PooledARWMH(ARWMH):
 
     # ------------------------------------------------------- the exchange --
     def _allreduce(self, buf: torch.Tensor, dev: int):
-        """all_reduce(sum) of one sums buffer.  RCCL: enqueued on the side
-        stream after the compute stream's work so far; returns the event the
-        consumer waits on.  gloo (ranks sharing a device, CPU tests): done
-        in place, host-synchronous; returns None."""
+        """all_reduce(sum) of one sums buffer.  RCCL without overlap: on the
+        compute stream itself (kernels_amd.distributed.rccl_allreduce_sum:
+        the update follows in stream order, no cross-stream event); returns
+        None.  RCCL with overlap: enqueued on the side stream after the
+        compute stream's work so far; returns the event the consumer waits
+        on.  gloo (ranks sharing a device, CPU tests): done in place,
+        host-synchronous; returns None."""
         if self._world() == 1 and not (self.force_collective and dist.is_available() and dist.is_initialized()):
             return None
         if dist.get_backend(self._group) != "nccl":
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self._group)
+            return None
+        if not self.overlap and not self.torch_stream_collective:
+            from .distributed import rccl_allreduce_sum, rccl_comm_ptr
+            if self._rccl_comm is None:
+                self._rccl_comm = rccl_comm_ptr(self._group, buf.device)
+            rccl_allreduce_sum(buf, self._rccl_comm, torch.cuda.current_stream(dev))
             return None
         if self._comm is None:
             self._comm = torch.cuda.Stream(device=dev)
@@ -248,12 +261,27 @@ class PooledARWMH(ARWMH):
         self._pending = (0, None)
         self._last_out = weakref.ref(state.z)
 
+    def check_device(self, synchronize: bool = True):
+        """Raise if a launch of this sampler flagged a device-side failure (the
+        d = 64 update's bounded wait ran out, so that update kept the shared
+        factor: amh_check_device).  synchronize=False reads the flag without
+        waiting, which covers every launch that has already finished; sample,
+        sample_ and run call it that way after each call (and run, which
+        synchronises anyway, with True); the handle's destruction reports what
+        is left as a RuntimeWarning."""
+        if self._handle is None:
+            return
+        if synchronize:
+            torch.cuda.synchronize(self._handle.device)
+        _lib.check(_lib.lib().amh_check_device(self._handle.h), self._handle.h)
+
     def sample(self, state, model_args=(), model_kwargs=None):
         """One pooled transition of every chain (sync_every > 1: one block of
         them); returns a new state."""
         self._check(state)
         out = self._new_like(state)
         self._one(state, out)
+        self.check_device(synchronize=False)
         return out
 
     def sample_(self, state, n_steps: int = 1):
@@ -270,9 +298,11 @@ class PooledARWMH(ARWMH):
                 _lib.check(L.amh_pooled_step_k(self._handle.h, C, ctypes.byref(c), ctypes.byref(c), int(n_steps), K,
                                                _lib.ptr(self._bufs[0]), _lib.stream_ptr(dev)), self._handle.h)
             self._sums = self._bufs[0]
+            self.check_device(synchronize=False)
             return state
         for _ in range(int(n_steps) // K):
             self._one(state, state)
+        self.check_device(synchronize=False)
         return state
 
     def run(self, state, n_steps: int, thinning: int = 1, collect_z: bool = True, collect_pe: bool = False):
@@ -305,6 +335,7 @@ class PooledARWMH(ARWMH):
                 cp[k].copy_(out.potential_energy)
         if int(n_steps) > done:
             self.sample_(out, int(n_steps) - done)
+        self.check_device(synchronize=True)
         return out, cz, cp
 
     def get_diagnostics_str(self, state):

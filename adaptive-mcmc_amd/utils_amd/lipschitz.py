@@ -41,8 +41,13 @@ TRAIN_LOG = None
 
 
 def _start_vector(W2: torch.Tensor) -> torch.Tensor:
-    """The power iteration's unit start vector for W2 (see spectral_norm)."""
-    seed = int(math.trunc(float(W2[0, 0].detach()))) & 0xFFFFFFFF
+    """The power iteration's unit start vector for W2 (see spectral_norm).  The
+    seed is jnp.uint32(W[0, 0]) as XLA converts a float to uint32: truncated
+    toward zero and SATURATED -- every value below 1 (negative ones included)
+    and NaN give 0, values from 2^32 up give 2^32 - 1.  (Parity unpinned: JAX
+    is not importable here; XLA's float-to-unsigned conversion saturates.)"""
+    w = float(W2[0, 0].detach())
+    seed = 0 if not w > 0.0 else min(int(math.trunc(w)), 0xFFFFFFFF)
     g = torch.Generator(device="cpu")
     g.manual_seed(seed)
     u = torch.randn(W2.shape[0], generator=g, dtype=W2.dtype).to(W2.device)
@@ -59,8 +64,8 @@ def spectral_norm(W: torch.Tensor, num_power_iters: int = 10, eps: float = 1e-10
     # every |W[0, 0]| < 1, so in the reference the power iteration starts from
     # the SAME vector at every training step (and the ten iterations, which
     # are differentiated through, under-estimate sigma in a way the optimiser
-    # can learn to use).  The same here: the seed is the truncated weight
-    # (two's complement for negative values), not its bit pattern.
+    # can learn to use).  The same here: the seed is the truncated,
+    # saturated weight (_start_vector), not its bit pattern.
     u = _start_vector(W2)
     v = torch.zeros(W2.shape[1], dtype=W.dtype, device=W.device)
     for _ in range(num_power_iters):

@@ -77,20 +77,40 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def lib_sha256() -> str | None:
+    """sha256 of the libamh.so this process loads (the build a profile came from)."""
+    import hashlib
+    from kernels_amd import _lib
+    try:
+        with open(_lib.LIB_PATH, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
+
+
 def measured_traffic(C: int, d: int):
-    """HBM bytes per launch of the step kernel from the newest committed PMC
-    summary for this workload (profiles/<round>_step_kernel.json, written by
-    tools/prof_summary.py from FETCH_SIZE/WRITE_SIZE passes of this bench)."""
+    """HBM bytes per launch of the step kernel from a committed PMC summary for
+    this workload (profiles/<tag>_step_kernel.json, written by
+    tools/prof_summary.py from FETCH_SIZE/WRITE_SIZE passes of this bench).
+    The summary of the library being measured (its `libamh_sha256`) is taken
+    when one exists; otherwise the newest by its own `created_utc` stamp (files
+    without one rank oldest, by tag).  Returns (bytes, path, same_build)."""
     import glob
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_step_kernel.json"))):
+    me = lib_sha256()
+    cands = []
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*_step_kernel.json")):
         try:
             j = json.load(open(f))
         except (OSError, ValueError):
             continue
         if j.get("chains") == C and j.get("dim") == d:
-            best = (j["traffic_bytes_per_launch"], os.path.relpath(f, ROOT))
-    return best
+            same = me is not None and j.get("libamh_sha256") == me
+            cands.append(((same, j.get("created_utc", ""), j.get("tag", "")), j["traffic_bytes_per_launch"],
+                          os.path.relpath(f, ROOT), same))
+    if not cands:
+        return None
+    best = max(cands, key=lambda c: c[0])
+    return best[1], best[2], best[3]
 
 
 def step_kernel_name(d: int) -> str:
@@ -328,7 +348,7 @@ def ess_leg(k, st, burn_in=20000, T=1000, headline_s_per_step=None):
     x = cz[:, :, coords].permute(1, 0, 2)  # [C, T, 4]
     vals = [float(v) for v in ess_of(x)]
     del x, cz
-    vals.append(float(ess_of(cp.t())))
+    vals.append(float(ess_of(cp.t())[0]))
     return {"ess_min": min(vals), "ess_per_s": min(vals) / el, "chains": C, "draws": T, "seconds": el,
             "ess_per_s_timing": ("ess_min / the wall time of the one FUSED run() launch that recorded the T "
                                  "draws (state in registers between steps)"),
@@ -696,7 +716,8 @@ def main():
         traffic = measured_traffic(C, d)
         roofline = {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic[0] if traffic else None,
-                    "traffic_source": traffic[1] if traffic else None, "kernel_ms": r["kern_ms"],
+                    "traffic_source": traffic[1] if traffic else None,
+                    "traffic_same_build": traffic[2] if traffic else None, "kernel_ms": r["kern_ms"],
                     "kernel": step_kernel_name(d),
                     "algorithmic_bytes_per_launch": per_launch_bytes}
         fused = None

@@ -108,6 +108,16 @@ const char* amh_last_error(const amh_handle* h);
 int amh_create(const amh_config* cfg, int device, amh_handle** out);
 int amh_destroy(amh_handle* h);
 
+/* A device-side failure flagged by a completed launch of this handle (the
+ * d = 64 pooled update's bounded wait running out: that update kept the shared
+ * factor, so the run no longer follows the bit spec).  Returns AMH_EHIP with
+ * the message in amh_last_error and clears the flag, else AMH_OK.  Reads a
+ * host-mapped word, no synchronisation: a launch still in flight is covered
+ * by a call after the caller has synchronised its stream (amh_destroy does
+ * that itself and returns the same code).  No counterpart in the reference,
+ * whose guards (arwmh.py:171, :191) cannot fail this way. */
+int amh_check_device(amh_handle* h);
+
 /* Model plug-in (arwmh.py:109-116 / the scripts' numpyro models).
  * data: device pointer, n_data floats; iparams model-specific:
  *   GAUSSIAN: none.  EIGHT_SCHOOLS: {J}.  KIDIQ: {N}.  DIAMONDS: {N, K}. */

@@ -108,6 +108,19 @@ __device__ __forceinline__ amh_u32x4 amh_philox4x32_10_unrolled(uint32_t c0, uin
 #define AMH_TAG_ASSS     0x53535341u /* ASSS per-step draws (c2 = 0: v, u_t,
                                         theta_0; c2 = 1: shrink uniforms)   */
 
+/* The step's noise stream (ARWMH.sample, arwmh.py:162-165, 174; round 5):
+ * words W_j = Philox4x32-10(c0 = j >> 2, c1 = ctr, c2 = 0, c3 = TAG_STEP;
+ * chain key).v[j & 3] for j = 0, 1, ..; the proposal noise is
+ * xi_r = N(W_r) for r < d and the accept uniform u = U(W_d) -- four words
+ * of every Philox call used, floor(d / 4) + 1 calls per chain-step (was one
+ * call per coordinate, three words discarded).  ctr is the stream position
+ * (state.i; the step index in sample_Pnx). */
+AMH_HD uint32_t amh_step_word(uint32_t j, uint32_t ctr, uint32_t k0, uint32_t k1) {
+  const amh_u32x4 o = amh_philox4x32_10(j >> 2, ctr, 0u, AMH_TAG_STEP, k0, k1);
+  const uint32_t q = j & 3u; /* selects, not an indexed load: no stack array on the device */
+  return (q == 0u) ? o.v[0] : ((q == 1u) ? o.v[1] : ((q == 2u) ? o.v[2] : o.v[3]));
+}
+
 /* 32 random bits -> float in [0,1): jax.random.uniform's construction
  * (mantissa fill of [1,2) then subtract 1). */
 AMH_HD float amh_unif01_from_bits(uint32_t b) {
@@ -224,6 +237,17 @@ AMH_HD float amh_normal_from_bits(uint32_t b) {
   float u = (f * 2.0f) + lo;     /* (hi - lo) rounds to 2 in fp32 */
   u = (u < lo) ? lo : u;
   return 1.41421356f * amh_erfinvf(u);
+}
+
+/* The whole step stream of one chain-step on the host (oracle): xi[0..d)
+ * and u, one Philox call per four words. */
+AMH_HD void amh_step_noise(int d, uint32_t ctr, uint32_t k0, uint32_t k1, float* xi, float* u) {
+  amh_u32x4 o = amh_philox4x32_10(0u, ctr, 0u, AMH_TAG_STEP, k0, k1);
+  for (int j = 0; j <= d; ++j) {
+    if (j > 0 && (j & 3) == 0) o = amh_philox4x32_10((uint32_t)(j >> 2), ctr, 0u, AMH_TAG_STEP, k0, k1);
+    if (j < d) xi[j] = amh_normal_from_bits(o.v[j & 3]);
+    else *u = amh_unif01_from_bits(o.v[j & 3]);
+  }
 }
 
 #if defined(__HIPCC__)

@@ -389,14 +389,8 @@ static int chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_t k1, 
   const int d = cfg->d;
   const int G = orc_gw(cfg);
   /* arwmh.py:162-165: proposal noise and accept uniform */
-  float xi[ORC_DMAX];
-  uint32_t ubits = 0;
-  for (int r = 0; r < d; ++r) {
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, ctr, 0u, AMH_TAG_STEP, k0, k1);
-    xi[r] = amh_normal_from_bits(o.v[0]);
-    if (r == 0) ubits = o.v[1];
-  }
-  const float u = amh_unif01_from_bits(ubits);
+  float xi[ORC_DMAX], u;
+  amh_step_noise(d, ctr, k0, k1, xi, &u); /* W_j = Philox(j >> 2, ctr)[j & 3]: xi_r = N(W_r), u = U(W_d) */
   /* arwmh.py:166-167: z' = z + (L e^lam + eps I) xi,  L xi = U (dl * xi) */
   const float el = amh_expf(s->lam);
   float eta[ORC_DMAX], zp[ORC_DMAX];
@@ -618,13 +612,8 @@ void orc_sample_pnx(const orc_cfg* cfg, const uint32_t* key, const float* x, int
     float pe = orc_potential1(cfg, z);
     const float el = amh_expf(log_step_size);
     for (int32_t t = 0; t < n; ++t) {
-      uint32_t ubits = 0;
-      for (int r = 0; r < d; ++r) {
-        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)t, 0u, AMH_TAG_STEP, keys[2 * c], keys[2 * c + 1]);
-        xi[r] = amh_normal_from_bits(o.v[0]);
-        if (r == 0) ubits = o.v[1];
-      }
-      const float u = amh_unif01_from_bits(ubits);
+      float u;
+      amh_step_noise(d, (uint32_t)t, keys[2 * c], keys[2 * c + 1], xi, &u);
       for (int r = 0; r < d; ++r) {
         float acc = 0.0f;
         for (int j = 0; j < d; ++j) acc = fmaf(A[r][j], xi[j], acc);
@@ -723,12 +712,22 @@ static int orc_pooled_big(const orc_cfg* cfg) {
 /* Pool every K (amh_pooled_stats_k): K transitions per chain with the frozen
  * shared state at noise positions i .. i+K-1, the sums over all K*C
  * chain-steps.  Lane-per-row path: one kernel, each wave's chains in order
- * with each chain's K steps in order.  MFMA path: K launch sequences, sums accumulated
- * in step order (sums = s_0, then sums + s_t). */
+ * with each chain's K steps in order.  MFMA path, d = 64: one launch, the
+ * chunk sums over (sub-chunk, step, chain) (orc_pooled_stats64_k); d > 64: K
+ * launch sequences, sums accumulated in step order (sums = s_0, then
+ * sums + s_t). */
+static void orc_pooled_stats64_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, const float* z,
+                                 const float* pe, const uint32_t* keys, const float* mu, const float* Lpacked,
+                                 float lam, float* z_out, float* pe_out, double* sums);
+
 void orc_pooled_stats_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, const float* z, const float* pe,
                         const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
                         float* z_out, float* pe_out, double* sums) {
   const int d = cfg->d;
+  if (orc_pooled_big(cfg) && d == 64) {
+    orc_pooled_stats64_k(cfg, C, i, K, z, pe, keys, mu, Lpacked, lam, z_out, pe_out, sums);
+    return;
+  }
   if (orc_pooled_big(cfg)) {
     const int64_t V = d + packed_size(d) + 2;
     double* tmp = (double*)malloc((size_t)V * sizeof(double));
@@ -771,13 +770,8 @@ void orc_pooled_stats_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, con
         for (int32_t s = 0; s < K; ++s) {
           cnt += 1.0;
           float xi[ORC_DMAX], zp[ORC_DMAX], delta[ORC_DMAX];
-          uint32_t ubits = 0;
-          for (int r = 0; r < d; ++r) {
-            const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)(i + s), 0u, AMH_TAG_STEP, k0, k1);
-            xi[r] = amh_normal_from_bits(o.v[0]);
-            if (r == 0) ubits = o.v[1];
-          }
-          const float u = amh_unif01_from_bits(ubits);
+          float u;
+          amh_step_noise(d, (uint32_t)(i + s), k0, k1, xi, &u);
           for (int r = 0; r < d; ++r) {
             float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             for (int j = 0; j < d; ++j) a4[j & 3] = fmaf(L[r][j], xi[j], a4[j & 3]);
@@ -1013,15 +1007,12 @@ static int big_step1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t* i_, 
   const int32_t it = i_[c];
   const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
   float xi[ORC_BIG], eta[ORC_BIG], acc[ORC_BIG], sa[ORC_BIG], sr[ORC_BIG], zp[ORC_BIG], wa[ORC_BIG], wr[ORC_BIG];
-  uint32_t ubits = 0;
+  float u;
+  amh_step_noise(d, (uint32_t)it, k0, k1, xi, &u);
   for (int r = 0; r < d; ++r) {
-    const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_STEP, k0, k1);
-    xi[r] = amh_normal_from_bits(o.v[0]);
-    if (r == 0) ubits = o.v[1];
     eta[r] = s->dl[r] * xi[r];
     acc[r] = sa[r] = sr[r] = 0.0f;
   }
-  const float u = amh_unif01_from_bits(ubits);
   const float el = amh_expf(lam[c]);
   /* propose pass */
   for (int j = 0; j < d; ++j) {
@@ -1175,13 +1166,8 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
     for (int64_t c = ch * chunk; c < C && c < (ch + 1) * chunk; ++c) {
       cnt += 1.0;
       const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
-      uint32_t ubits = 0;
-      for (int r = 0; r < d; ++r) {
-        const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)i, 0u, AMH_TAG_STEP, k0, k1);
-        xi[r] = amh_normal_from_bits(o.v[0]);
-        if (r == 0) ubits = o.v[1];
-      }
-      const float u = amh_unif01_from_bits(ubits);
+      float u;
+      amh_step_noise(d, (uint32_t)i, k0, k1, xi, &u);
       for (int r = 0; r < d; ++r) {
         float acc = 0.0f;
         const int kend = 32 * (r / 32 + 1);
@@ -1207,6 +1193,88 @@ static void orc_pooled_stats_big(const orc_cfg* cfg, int64_t C, int32_t i, const
         for (int k = 0; k <= r; ++k) S[r * d + k] = fmaf(dl[r], dl[k], S[r * d + k]);
       }
       sa = sa + alpha;
+    }
+    double* acc = part + ch * V;
+    for (int r = 0; r < d; ++r) acc[r] = (double)sd[r];
+    for (int k = 0; k < d; ++k)
+      for (int r = k; r < d; ++r) acc[d + col_off(d, k) + (r - k)] = (double)S[r * d + k];
+    acc[d + P] = (double)sa;
+    acc[d + P + 1] = cnt;
+    free(S);
+  }
+  const int64_t n_groups = (n_chunks + 15) / 16;
+  for (int64_t v = 0; v < V; ++v) {
+    double tot = 0.0;
+    for (int64_t g = 0; g < n_groups; ++g) {
+      double s = 0.0;
+      for (int64_t c2 = g * 16; c2 < n_chunks && c2 < (g + 1) * 16; ++c2) s += part[c2 * V + v];
+      tot += s;
+    }
+    sums[v] = tot;
+  }
+  free(part);
+}
+
+/* d = 64 (pooled_fused64_kernel, round 5): the K steps of a block run in one
+ * launch.  Each 128-chain chunk is two 64-chain sub-chunks; the chunk's
+ * float32 sums run over its chain-steps in the order (sub-chunk, step, chain)
+ * -- sub-chunk 0's K steps chain by chain, then sub-chunk 1's -- and the
+ * chunks are reduced in double as for one step.  K = 1 is the per-step order
+ * of orc_pooled_stats_big. */
+static void orc_pooled_stats64_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, const float* z,
+                                 const float* pe, const uint32_t* keys, const float* mu, const float* Lpacked,
+                                 float lam, float* z_out, float* pe_out, double* sums) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const int64_t V = d + P + 2;
+  const int64_t chunk = orc_big_chunk(d), sub = 64;
+  const int64_t n_chunks = (C + chunk - 1) / chunk;
+  const float el = amh_expf(lam);
+  double* part = (double*)calloc((size_t)(n_chunks * V), sizeof(double));
+  for (int64_t c = 0; c < C; ++c) {
+    for (int r = 0; r < d; ++r) z_out[c * d + r] = z[c * d + r];
+    pe_out[c] = pe[c];
+  }
+#pragma omp parallel for schedule(dynamic, 1)
+  for (int64_t ch = 0; ch < n_chunks; ++ch) {
+    float* S = (float*)calloc((size_t)d * d, sizeof(float));
+    float sd[ORC_BIG], xi[ORC_BIG], zp[ORC_BIG], dl[ORC_BIG];
+    float sa = 0.0f;
+    double cnt = 0.0;
+    for (int r = 0; r < d; ++r) sd[r] = 0.0f;
+    for (int64_t s0 = ch * chunk; s0 < C && s0 < (ch + 1) * chunk; s0 += sub) {
+      for (int32_t t = 0; t < K; ++t) {
+        for (int64_t c = s0; c < C && c < s0 + sub; ++c) {
+          cnt += 1.0;
+          float* zc = z_out + c * d;
+          float u;
+          amh_step_noise(d, (uint32_t)(i + t), keys[2 * c], keys[2 * c + 1], xi, &u);
+          for (int r = 0; r < d; ++r) {
+            float acc = 0.0f;
+            const int kend = 32 * (r / 32 + 1);
+            for (int k = 0; k < kend; ++k) {
+              const float lrk = (k <= r) ? Lpacked[col_off(d, k) + (r - k)] : 0.0f;
+              acc = fmaf(lrk, xi[k], acc);
+            }
+            zp[r] = zc[r] + fmaf(el, acc, cfg->eps * xi[r]);
+          }
+          float pep = pot_gaussian_big(cfg, zp);
+          if (amh_isnan(pep)) pep = INFINITY;
+          const float ex = amh_expf(pe_out[c] - pep);
+          const float alpha = (ex > 1.0f) ? 1.0f : ex;
+          const int accept = u < alpha;
+          for (int r = 0; r < d; ++r) {
+            if (accept) zc[r] = zp[r];
+            dl[r] = zc[r] - mu[r];
+          }
+          if (accept) pe_out[c] = pep;
+          for (int r = 0; r < d; ++r) {
+            sd[r] = sd[r] + dl[r];
+            for (int k = 0; k <= r; ++k) S[r * d + k] = fmaf(dl[r], dl[k], S[r * d + k]);
+          }
+          sa = sa + alpha;
+        }
+      }
     }
     double* acc = part + ch * V;
     for (int r = 0; r < d; ++r) acc[r] = (double)sd[r];
@@ -1298,6 +1366,10 @@ static int orc_pooled_update_big(const orc_cfg* cfg, const double* sums, int32_t
 }
 
 /* ================================================================= ASSS ==== */
+/* Test hook (tests/test_asss.py): treat every tangent as zero-norm. */
+int orc_test_zero_tangent = 0;
+void orc_set_test_zero_tangent(int on) { orc_test_zero_tangent = on; }
+
 /* asss.py:197-251 (ASSS.sample), kernel mirror of amh_asss.hip: the chain is
  * held as (U, dl) between the steps of one launch like chain_t; the factor
  * is written back as U diag(dl) if any step updated it, else verbatim.
@@ -1348,9 +1420,14 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
   for (int r = 0; r < d; ++r) v[r] = fmaf(-dot, zr[r], v[r]); /* one rounding: no exact cancellation */
   vd = fmaf(-dot, zd, vd);
   for (int r = 0; r < G; ++r) t[r] = (r < d) ? v[r] * v[r] : 0.0f;
-  const float nv = sqrtf(group_sum(t, G) + (vd * vd));
-  for (int r = 0; r < d; ++r) v[r] = v[r] / nv;
-  vd = vd / nv;
+  float nv = sqrtf(group_sum(t, G) + (vd * vd));
+  if (orc_test_zero_tangent) nv = 0.0f; /* test hook: the measure-zero case, on demand */
+  /* |v| = 0 (every component rounded to 0; the reference's v / norm(v) is
+   * NaN): theta = 0, the shrinkage's own fallback (asss.py:94) -- the state
+   * is kept (re-projected) and the adaptation runs as usual */
+  const int degen = !(nv > 0.0f);
+  for (int r = 0; r < d; ++r) v[r] = degen ? 0.0f : v[r] / nv;
+  vd = degen ? 0.0f : vd / nv;
   /* S z_1d and S v_1d */
   float Sz[ORC_DMAX], Sv[ORC_DMAX], hz[ORC_DMAX], hv[ORC_DMAX];
   for (int j = 0; j < d; ++j) { hz[j] = e[j] * zr[j]; hv[j] = e[j] * v[j]; }
@@ -1386,7 +1463,7 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
     ux = orc_potential1(cfg, xt);
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
-    cont = (pt > tpe) || (om < cfg->eps);
+    cont = !degen && ((pt > tpe) || (om < cfg->eps));
   }
   while (cont) {
     if (th < 0.0f) thmin = th;
@@ -1403,7 +1480,7 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
     iter += 1;
     cont = (iter < 50) && ((pt > tpe) || (om < cfg->eps));
   }
-  const int capped = iter >= 50;
+  const int capped = degen || iter >= 50;
   float xn[ORC_DMAX];
   for (int r = 0; r < d; ++r) xn[r] = capped ? x0[r] : xt[r];
   float pen = capped ? U0 : ux;

@@ -80,12 +80,16 @@ def chain_keys(key, chain_offset, n):
 
 def step_noise(keys, ctr, d):
     """Per-chain proposal noise bits [C, d] and accept-uniform bits [C] for a step at
-    stream position ctr (= state.i for ARWMH.sample)."""
+    stream position ctr (= state.i for ARWMH.sample): the words
+    W_j = Philox(j >> 2, ctr, 0, TAG_STEP; key)[j & 3], xi_r from W_r (r < d),
+    u from W_d (include/amh_math.h amh_step_word)."""
     keys = np.asarray(keys, np.uint32).reshape(-1, 2)
-    r = np.arange(d, dtype=np.uint32)[None, :]
+    nc = d // 4 + 1
+    c = np.arange(nc, dtype=np.uint32)[None, :]
     ctr = np.broadcast_to(np.asarray(ctr, np.uint32).reshape(-1, 1), (keys.shape[0], 1))
-    o = philox4x32_10(r, ctr, 0, TAG_STEP, keys[:, 0:1], keys[:, 1:2])
-    return o[0], o[1][:, 0]
+    o = philox4x32_10(c, ctr, 0, TAG_STEP, keys[:, 0:1], keys[:, 1:2])
+    words = np.stack(o, axis=-1).reshape(keys.shape[0], 4 * nc)  # W_j at [:, j]
+    return words[:, :d], words[:, d]
 
 
 # ------------------------------------------------------------ cholupdate --

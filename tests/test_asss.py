@@ -91,3 +91,30 @@ def test_gaussian_moments(orc):
     x = cz[::4].reshape(-1, 4).astype(np.float64)
     assert np.abs(x.mean(0)).max() < 0.05
     np.testing.assert_allclose(np.cov(x.T), np.linalg.inv(g.precision), atol=0.08)
+
+
+def test_zero_norm_tangent_keeps_state(orc):
+    """A tangent that rounds to zero in every component (|v| = 0: the
+    reference's v / norm(v) is NaN, asss.py:222, and would poison the chain)
+    takes the shrinkage's own fallback, theta = 0 (asss.py:94): x' is x
+    re-projected through the sphere, U(x') its potential, and the adaptation
+    runs with delta = x' - mu.  Forced here with the oracle's test hook (the
+    event is measure-zero after the fmaf projection); the kernel
+    (amh_asss.h) makes the same decisions."""
+    from kernels_amd import PRNGKey
+    _, _, om = make_case("gaussian", 12)
+    st = orc.init(om, PRNGKey(3), 16)
+    orc.asss_step(om, st, 5)
+    before = st.copy()
+    L = orc.lib()
+    L.orc_set_test_zero_tangent(1)
+    try:
+        orc.asss_step(om, st, 1)
+    finally:
+        L.orc_set_test_zero_tangent(0)
+    assert np.all(np.isfinite(st.z)) and np.all(np.isfinite(st.potential_energy))
+    assert np.all(np.isfinite(st.scale)) and np.all(np.isfinite(st.loc))
+    np.testing.assert_allclose(st.z, before.z, rtol=1e-5, atol=1e-5)  # kept, up to the re-projection
+    np.testing.assert_allclose(st.potential_energy, orc.potential(om, st.z), rtol=1e-6)
+    assert np.all(st.i == before.i + 1)
+    assert not np.array_equal(st.loc, before.loc)  # adaptation ran

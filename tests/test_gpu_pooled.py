@@ -46,7 +46,10 @@ def _run(kind, d, C, steps, gpu, orc, seed=0, K=1):
                                             ("gaussian", 7, 517, 8), ("eight_schools", None, 64, 8),
                                             ("kidiq", None, 100, 5), ("diamonds", None, 40, 3),
                                             ("diamonds_ss", None, 1000, 4),
-                                            ("gaussian", 128, 700, 4), ("gaussian", 256, 600, 3)])
+                                            ("gaussian", 128, 700, 4), ("gaussian", 256, 600, 3),
+                                            # 3, 5 and 7 column tiles of the d > 64 update
+                                            ("gaussian", 96, 500, 3), ("gaussian", 160, 400, 3),
+                                            ("gaussian", 224, 300, 3)])
 def test_pooled_bitexact(kind, d, C, steps, gpu, orc):
     _run(kind, d, C, steps, gpu, orc)
 
@@ -123,7 +126,8 @@ def test_pooled_blocks_bitexact(kind, d, C, blocks, K, gpu, orc):
     _run(kind, d, C, blocks, gpu, orc, K=K)
 
 
-@pytest.mark.parametrize("d,C,K", [(16, 999, 4), (128, 300, 3), (64, 70000, 4), (64, 70000, 1)])
+@pytest.mark.parametrize("d,C,K", [(16, 999, 4), (128, 300, 3), (64, 70000, 4), (64, 70000, 1),
+                                   (96, 300, 4), (160, 260, 3), (224, 200, 2)])
 def test_pooled_blocks_inplace(d, C, K, gpu, orc):
     """sample_(12) with sync_every = K in place (amh_pooled_step_k) equals
     12 / K out-of-place block samples."""
@@ -346,18 +350,21 @@ def test_pooled_keep_factor_when_not_pd(d, C, gpu, orc):
             assert a.tobytes() == np.asarray(b).astype(a.dtype).tobytes(), f"{name} differs at step {t + 1}"
 
 
-def test_rccl_branch_one_rank_bitexact():
-    """The RCCL exchange (pooled.py _allreduce: the side stream, the event the
-    compute stream waits on) in a 1-rank `nccl` group, forced on one GPU, is
-    bit-equal to the fused one-rank path (tools/rccl_one_rank.py, its own
-    process so this process keeps no process group)."""
+@pytest.mark.parametrize("K", [1, 16])
+def test_rccl_branch_one_rank_bitexact(K):
+    """The RCCL exchange in a 1-rank `nccl` group, forced on one GPU: RCCL on
+    the compute stream (pooled.py _allreduce, distributed.rccl_allreduce_sum)
+    and through torch.distributed's side stream are both bit-equal to the
+    fused one-rank path, per step and with sync_every = 16
+    (tools/rccl_one_rank.py, its own process so this process keeps no process
+    group)."""
     import os
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_one_rank.py"), "65536", "64", "20"],
-                       capture_output=True, text=True, timeout=240, env=env)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_one_rank.py"), "65536", "64",
+                        "20" if K == 1 else "32", str(K)], capture_output=True, text=True, timeout=240, env=env)
     print(r.stdout[-2000:], r.stderr[-2000:])
     assert r.returncode == 0
     assert "bit-equal to the fused path" in r.stdout

@@ -129,16 +129,19 @@ def test_kernel_distance_1d_notebook_cell101(gpu):
 
 
 def test_power_iteration_start_is_fixed_like_fold_in():
-    """lipschitz.py:30 folds jnp.uint32(W[0, 0]) into PRNGKey(0): every weight
-    with |W[0, 0]| < 1 starts the power iteration from the same vector (the
-    same at every training step), a different integer part from another."""
+    """lipschitz.py:27 folds jnp.uint32(W[0, 0]) into PRNGKey(0): XLA's
+    float-to-uint32 conversion truncates and saturates, so every weight below
+    1 -- negative ones included -- starts the power iteration from the same
+    vector (the same at every training step), a different integer part from
+    another, and 2^32 or more from the last seed."""
     g = torch.Generator().manual_seed(3)
     W = torch.randn(32, 32, generator=g) * 0.2
     starts = []
-    for w00 in (0.3, -0.7, 0.0, 0.999, 1.5, 2.2):
+    for w00 in (0.3, -0.7, 0.0, 0.999, -1.5, -3.0, float("nan"), 1.5, 2.2, 5e9, 2.0 ** 32 - 1):
         W[0, 0] = w00
         starts.append(Lz._start_vector(W))
-    for u in starts[1:4]:
+    for u in starts[1:7]:
         assert torch.equal(u, starts[0])
-    assert not torch.equal(starts[4], starts[0]) and not torch.equal(starts[5], starts[4])
+    assert not torch.equal(starts[7], starts[0]) and not torch.equal(starts[8], starts[7])
+    assert torch.equal(starts[9], starts[10]) and not torch.equal(starts[9], starts[8])
     assert float(torch.linalg.norm(starts[0])) == pytest.approx(1.0, rel=1e-6)

@@ -183,12 +183,14 @@ def _shared_copy(sh):
 
 
 @pytest.mark.parametrize("kind,d,C,K", [("gaussian", 12, 37, 4), ("eight_schools", None, 70, 3),
-                                        ("gaussian", 128, 40, 3)])
+                                        ("gaussian", 128, 40, 3), ("gaussian", 64, 300, 5)])
 def test_block_is_k_frozen_steps(kind, d, C, K, orc):
     """A block of K transitions (orc_pooled_stats_k) is K single pooled steps
     with the shared state frozen: per-chain z / pe bit for bit, the sums equal
-    up to association order (d <= 64: one float32 accumulator per wave over
-    all K steps; d > 64: the per-step sums added in step order, exactly)."""
+    up to association order (d < 64: one float32 accumulator per wave over
+    all K steps; d = 64: one per 128-chain chunk over (sub-chunk, step, chain),
+    orc_pooled_stats64_k; d > 64: the per-step sums added in step order,
+    exactly)."""
     from helpers import make_case
     from kernels_amd import PRNGKey
     _, _, om = make_case(kind, d)

@@ -16,6 +16,7 @@ moved by 16 B/lane buffer_load...lds -- so it is doubled.
   python tools/prof_summary.py r2 [--steps 200 --pmc-steps 20]
 """
 import argparse
+import datetime
 import csv
 import json
 import os
@@ -28,6 +29,16 @@ KERNEL = "arwmh_step64_kernel"  # the d = 64 specialisation (amh_kernels.hip)
 
 def step_rows(path):
     return [r for r in csv.DictReader(open(path)) if KERNEL in r["Kernel_Name"]]
+
+
+def lib_sha256():
+    import hashlib
+    p = os.path.join(ROOT, "adaptive-mcmc_amd", "lib", "libamh.so")
+    try:
+        with open(p, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
 def main():
@@ -82,6 +93,10 @@ def main():
         "traffic_over_algorithmic": traffic / (2 * alg_read),
         "chains": C,
         "dim": d,
+        # which build this is (bench.py measured_traffic matches it against
+        # the library it loads) and when it was summarised
+        "libamh_sha256": lib_sha256(),
+        "created_utc": datetime.datetime.now(datetime.timezone.utc).strftime("%Y-%m-%dT%H:%M:%SZ"),
     }
     with open(os.path.join(dst, f"{a.tag}_step_kernel.json"), "w") as f:
         json.dump(out, f, indent=1)
