@@ -34,6 +34,7 @@ namespace amh {
 namespace {
 
 constexpr int kNS = 4;  // row slots per lane: d <= 64 * kNS
+constexpr int kAsssBigMaxIter = 50;  // asss.py:59 max_iterations
 
 __device__ __forceinline__ float rdl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -539,6 +540,406 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
   }
 }
 
+// ------------------------------------------------------------------ ASSS ----
+// ASSS (asss.py:192-269) for 64 < d <= 256, d % 32 == 0, dense Gaussian:
+// one wave per chain, lane l owns rows 64 s + l, the factor streamed column
+// by column through the wave's LDS double buffer (for_columns).  Four passes
+// over the factor per transition (bit spec: oracle asss_step_big1):
+//   A  y = S^-1 (x - mu), S = (L + eps I) sqrt(d): at column j lane j's
+//      y_j = b_j / D_j and g = y_j e_j go to every lane, rows r > j take
+//      b_r = fmaf(-U_rj, g, b_r)                            (asss.py:33-45)
+//   B  a = S z, b = S v: one accumulator per row in column order, the
+//      diagonal (U_rr = 1) at column r, then + eps sqrt(d) (z_r, v_r)
+//   -- the potential along the slice circle: Pa, Pb, Pg = P a, P b, P g
+//      (g = mu - m; P's rows read coalesced, an fmaf chain over k), then
+//      every shrink step is O(d): D = (a c + b s) / om + g, Y = (Pa c + Pb s)
+//      / om + Pg, U = 0.5 sum D Y + c0                      (asss.py:59-96)
+//   C  w = U^-1 delta            D  the rank-one update streaming L' out,
+//      as the large-d ARWMH step pass (no step size)   (asss.py:246-267)
+// ADAPT = false is the frozen kernel of sample_Pnx (shared loc / factor).
+namespace {
+
+template <bool ADAPT>
+__device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, const float (&dl)[kNS],
+                                               const float (&inv)[kNS], float (&x)[kNS], float (&mu)[kNS],
+                                               float& pe, float& asc, int32_t it, uint32_t k0, uint32_t k1, int d,
+                                               int64_t P, float eps, int32_t W, float gamma_in, const ModelArgs& model,
+                                               float* wb0, float* wb1, int lane) {
+  const float* m = model.data;
+  const float* Pm = model.data + d;
+  const float c0 = model.data[d + d * d];
+  const float sd = sqrtf((float)d);
+  const float epsd = eps * sd;
+  const float fd = (float)d;
+  // ---- draws (asss.py:207, 219, 225, 60): the d <= 64 kernel's stream
+  float v[kNS];
+  static_for<kNS>([&](auto K) {
+    const int r = 64 * K + lane;
+    v[K] = (r < d) ? amh_normal_from_bits(amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_ASSS, k0, k1).v[0])
+                   : 0.0f;
+  });
+  const amh_u32x4 o0 = amh_philox4x32_10(0u, (uint32_t)it, 0u, AMH_TAG_ASSS, k0, k1);
+  float vd = amh_normal_from_bits(o0.v[1]);
+  const float ut = amh_unif01_from_bits(o0.v[2]);
+  const float th0 = 6.28318548f * amh_unif01_from_bits(o0.v[3]);
+  // ---- pass A: y = S^-1 (x - mu)
+  float e[kNS], invD[kNS], b[kNS], y[kNS], tt[kNS];
+  static_for<kNS>([&](auto K) {
+    const bool act = 64 * K + lane < d;
+    e[K] = dl[K] * sd;
+    invD[K] = 1.0f / ((dl[K] + eps) * sd);
+    b[K] = act ? x[K] - mu[K] : 0.0f;
+    y[K] = 0.0f;
+  });
+  for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+    constexpr int kb = KB;
+    const int jl = j - 64 * kb;
+    const float yl = rdl(b[kb] * invD[kb], jl);
+    const float g = yl * rdl(e[kb], jl);
+    const float invj = rdl(inv[kb], jl);
+    if (lane == jl) y[kb] = yl;
+    static_for<kNS>([&](auto K) {
+      if constexpr (K >= kb) {
+        const int r = 64 * K + lane;
+        if (r > j && r < d) b[K] = fmaf(-(vv[K] * invj), g, b[K]);
+      }
+    });
+  });
+  // ---- stereographic projection, tangent v (asss.py:40-45, 219-222)
+  static_for<kNS>([&](auto K) { tt[K] = y[K] * y[K]; });
+  const float ns = big_sum(tt);
+  const float den = ns + 1.0f;
+  float zr[kNS];
+  static_for<kNS>([&](auto K) { zr[K] = (2.0f * y[K]) / den; });
+  const float zd = (ns - 1.0f) / den;
+  static_for<kNS>([&](auto K) { tt[K] = v[K] * zr[K]; });
+  const float dot = big_sum(tt) + (vd * zd);
+  static_for<kNS>([&](auto K) { v[K] = (64 * K + lane < d) ? fmaf(-dot, zr[K], v[K]) : 0.0f; });
+  vd = fmaf(-dot, zd, vd);
+  static_for<kNS>([&](auto K) { tt[K] = v[K] * v[K]; });
+  const float nv = sqrtf(big_sum(tt) + (vd * vd));
+  const bool degen = !(nv > 0.0f);  // the d <= 64 kernel's rule (amh_asss.h)
+  static_for<kNS>([&](auto K) { v[K] = degen ? 0.0f : v[K] / nv; });
+  vd = degen ? 0.0f : vd / nv;
+  // ---- pass B: a = S z, b = S v
+  float hz[kNS], hv[kNS], a[kNS], bb[kNS];
+  static_for<kNS>([&](auto K) {
+    hz[K] = e[K] * zr[K];
+    hv[K] = e[K] * v[K];
+    a[K] = bb[K] = 0.0f;
+  });
+  for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+    constexpr int kb = KB;
+    const int jl = j - 64 * kb;
+    const float hzj = rdl(hz[kb], jl), hvj = rdl(hv[kb], jl), invj = rdl(inv[kb], jl);
+    if (lane == jl) {
+      a[kb] = fmaf(1.0f, hzj, a[kb]);
+      bb[kb] = fmaf(1.0f, hvj, bb[kb]);
+    }
+    static_for<kNS>([&](auto K) {
+      if constexpr (K >= kb) {
+        const int r = 64 * K + lane;
+        if (r > j && r < d) {
+          const float uo = vv[K] * invj;
+          a[K] = fmaf(uo, hzj, a[K]);
+          bb[K] = fmaf(uo, hvj, bb[K]);
+        }
+      }
+    });
+  });
+  float Sz[kNS], Sv[kNS], gm[kNS], Pa[kNS], Pb[kNS], Pg[kNS];
+  static_for<kNS>([&](auto K) {
+    const int r = 64 * K + lane;
+    const bool act = r < d;
+    Sz[K] = a[K] + epsd * zr[K];
+    Sv[K] = bb[K] + epsd * v[K];
+    gm[K] = act ? mu[K] - m[act ? r : 0] : 0.0f;
+    Pa[K] = Pb[K] = Pg[K] = 0.0f;
+  });
+  // ---- P a, P b, P g: row k of P (= column k) coalesced, k in order
+  static_for<kNS>([&](auto KB) {
+    constexpr int kb = KB;
+    if (64 * kb < d) {
+      const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;  // a multiple of 32
+      for (int k2 = 0; k2 < kmax; k2 += 8) {
+        float pr[8][kNS];
+        static_for<8>([&](auto T) {
+          const float* row = Pm + (int64_t)(64 * kb + k2 + T) * d;
+          static_for<kNS>([&](auto K) { pr[T][K] = (64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+        });
+        static_for<8>([&](auto T) {
+          const int kl = k2 + T;
+          const float sa = rdl(Sz[kb], kl), sb = rdl(Sv[kb], kl), sg = rdl(gm[kb], kl);
+          static_for<kNS>([&](auto K) {
+            Pa[K] = fmaf(pr[T][K], sa, Pa[K]);
+            Pb[K] = fmaf(pr[T][K], sb, Pb[K]);
+            Pg[K] = fmaf(pr[T][K], sg, Pg[K]);
+          });
+        });
+      }
+    }
+  });
+  // the point at angle (cs, sn) of the slice circle: x and U
+  auto eval = [&](float cs, float sn, float (&xo)[kNS], float& om) -> float {
+    om = 1.0f - ((zd * cs) + (vd * sn));
+    float t4[kNS];
+    static_for<kNS>([&](auto K) {
+      const bool act = 64 * K + lane < d;
+      const float num = (Sz[K] * cs) + (Sv[K] * sn);
+      const float Dr = (num / om) + gm[K];
+      const float Yr = (((Pa[K] * cs) + (Pb[K] * sn)) / om) + Pg[K];
+      t4[K] = act ? Dr * Yr : 0.0f;
+      xo[K] = act ? (num / om) + mu[K] : 0.0f;
+    });
+    return (0.5f * big_sum(t4)) + c0;
+  };
+  // ---- slice level and shrinkage (asss.py:216-239, 59-96)
+  float x0[kNS], xt[kNS], om0;
+  const float U0 = eval(1.0f, 0.0f, x0, om0);
+  const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
+  float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
+  int32_t iter = 0;
+  float ux;
+  bool cont;
+  {
+    float sn, cs, om;
+    amh_sincosf(th, &sn, &cs);
+    ux = eval(cs, sn, xt, om);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    cont = !degen && ((pt > tpe) || (om < eps));
+  }
+  while (cont) {  // wave-uniform: one chain per wave
+    if (th < 0.0f) thmin = th;
+    if (th >= 0.0f) thmax = th;
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)iter, (uint32_t)it, 1u, AMH_TAG_ASSS, k0, k1);
+    th = thmin + (thmax - thmin) * amh_unif01_from_bits(o.v[0]);
+    float sn, cs, om;
+    amh_sincosf(th, &sn, &cs);
+    ux = eval(cs, sn, xt, om);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    iter += 1;
+    cont = (iter < kAsssBigMaxIter) && ((pt > tpe) || (om < eps));
+  }
+  const bool capped = degen || iter >= kAsssBigMaxIter;  // asss.py:94: theta = 0
+  float xn[kNS];
+  static_for<kNS>([&](auto K) { xn[K] = capped ? x0[K] : xt[K]; });
+  float pen = capped ? U0 : ux;
+  if (amh_isnan(pen)) pen = INFINITY;
+  if constexpr (!ADAPT) {
+    static_for<kNS>([&](auto K) { x[K] = xn[K]; });
+    pe = pen;
+    (void)Lout;
+    (void)W;
+    (void)gamma_in;
+    (void)asc;
+    return;
+  } else {
+    // ---- adaptation (asss.py:246-267): mean, rank-one update, as_change
+    const float gamma = gamma_in;
+    float delta[kNS], mun[kNS], Dg[kNS], one[kNS], ws[kNS], sw[kNS], gw2[kNS];
+    const float sq = sqrtf(1.0f - gamma);
+    static_for<kNS>([&](auto K) {
+      const bool act = 64 * K + lane < d;
+      delta[K] = act ? xn[K] - mu[K] : 0.0f;
+      mun[K] = act ? mu[K] + gamma * delta[K] : 0.0f;
+      const float dm = mun[K] - mu[K];
+      tt[K] = act ? dm * dm : 0.0f;
+      const float ajj = sq * dl[K];
+      Dg[K] = ajj * ajj;
+      one[K] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+      sw[K] = ws[K] = 0.0f;
+    });
+    const float locd = sqrtf(big_sum(tt));
+    // pass C: w = U^-1 delta
+    for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      constexpr int kb = KB;
+      const int jl = j - 64 * kb;
+      const float wj = rdl(delta[kb] - sw[kb], jl);
+      const float invj = rdl(inv[kb], jl);
+      if (lane == jl) ws[kb] = wj;
+      static_for<kNS>([&](auto K) {
+        if constexpr (K >= kb) {
+          const int r = 64 * K + lane;
+          if (r > j && r < d) sw[K] = fmaf(vv[K] * invj, wj, sw[K]);
+        }
+      });
+    });
+    float cc[kNS], qq[kNS];
+    bool bad = false;
+    {
+      float carry = 0.0f;
+      static_for<kNS>([&](auto K) {
+        const bool act = 64 * K + lane < d;
+        gw2[K] = act ? gamma * (ws[K] * ws[K]) : 0.0f;
+        const float t = act ? gw2[K] / Dg[K] : 0.0f;
+        const float ex = Grp<64>::excl_scan(t, lane);
+        const float bs = (K == 0) ? ex : ex + carry;
+        const float tot = rdl(ex + t, 63);
+        carry = (K == 0) ? tot : carry + tot;
+        const float bq = 1.0f + bs;
+        const float g2 = (bq * Dg[K]) + gw2[K];
+        const float dn = g2 / bq;
+        cc[K] = (gamma * ws[K]) / g2;
+        qq[K] = sqrtf(dn);
+        const float dnew = fmaf(cc[K], 0.0f, one[K]) * qq[K];
+        bad = bad || (act && amh_isnan(dnew));
+      });
+    }
+    const bool revert = __ballot(bad) != 0ull;
+    float sdiff = 0.0f;
+    if (!revert) {
+      // pass D: the update, L' streamed out (in place allowed: block b + 1 is
+      // in flight before block b's columns are written)
+      float ac[kNS], bc[kNS], sv[kNS], sacc[kNS];
+      static_for<kNS>([&](auto K) {
+        ac[K] = qq[K] - dl[K];
+        bc[K] = cc[K] * qq[K];
+        sv[K] = sacc[K] = 0.0f;
+      });
+      for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+        constexpr int kb = KB;
+        const int jl = j - 64 * kb;
+        const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
+        const float bcj = rdl(bc[kb], jl), invj = rdl(inv[kb], jl), qj = rdl(qq[kb], jl);
+        float* ocol = Lout + col_off(d, j) - j;
+        if (lane == jl) {
+          const float t0 = fmaf(1.0f, acj, bcj * 0.0f);
+          sacc[kb] = fmaf(t0, t0, sacc[kb]);
+          ocol[j] = 1.0f * qj;
+        }
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r > j && r < d) {
+              const float uo = vv[K] * invj;
+              sv[K] = fmaf(uo, wsj, sv[K]);
+              const float w = delta[K] - sv[K];
+              const float un = fmaf(cj, w, uo);
+              const float t1 = fmaf(uo, acj, bcj * w);
+              sacc[K] = fmaf(t1, t1, sacc[K]);
+              ocol[r] = un * qj;
+            }
+          }
+        });
+      });
+      sdiff = sqrtf(big_sum(sacc));
+    } else if (Lout != Lc) {  // factor kept (asss.py:255): copied verbatim
+      for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+        constexpr int kb = KB;
+        float* ocol = Lout + col_off(d, j) - j;
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r >= j && r < d) ocol[r] = vv[K];
+          }
+        });
+      });
+    }
+    asc = locd + sdiff;
+    static_for<kNS>([&](auto K) {
+      x[K] = xn[K];
+      mu[K] = mun[K];
+    });
+    pe = pen;
+  }
+}
+
+}  // namespace
+
+// ASSS.sample: one transition of every chain per launch (host loops n_steps)
+__global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
+  extern __shared__ float lds_big[];
+  const int d = p.d;
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb0 = lds_big + (size_t)wv * 2 * kColBlk * d;
+  float* wb1 = wb0 + kColBlk * d;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  typedef __attribute__((address_space(4))) const float cf;
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
+    const float* Lc = p.in.scale + c * P;
+    float* Lo = p.out.scale + c * P;
+    const int32_t it = p.in.i[c];
+    const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
+    float dl[kNS], inv[kNS], x[kNS], mu[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      dl[K] = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
+      inv[K] = (amh_isfinite(dl[K]) && dl[K] != 0.0f) ? 1.0f / dl[K] : 0.0f;
+      x[K] = act ? p.in.z[c * d + r] : 0.0f;
+      mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
+    });
+    const int32_t itr = it + 1;
+    const int32_t n = (it < p.W) ? itr : itr - p.W;
+    const float gamma = (n < p.gamma_tab_n) ? ((const cf*)p.gamma_tab)[n] : amh_lr_gamma(n, p.a);
+    float pe = p.in.potential_energy[c];
+    float asc = 0.0f;
+    asss_big_chain<true>(Lc, Lo, dl, inv, x, mu, pe, asc, it, k0, k1, d, P, p.eps, p.W, gamma, p.model, wb0, wb1,
+                         lane);
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) {
+        p.out.z[c * d + r] = x[K];
+        p.out.loc[c * d + r] = mu[K];
+        if (p.col_z != nullptr) p.col_z[c * d + r] = x[K];
+      }
+    });
+    if (lane == 0) {
+      p.out.i[c] = itr;
+      p.out.potential_energy[c] = pe;
+      p.out.as_change[c] = asc;
+      p.out.rng_key[2 * c] = k0;
+      p.out.rng_key[2 * c + 1] = k1;
+      if (p.col_pe != nullptr) p.col_pe[c] = pe;
+    }
+  }
+}
+
+// ASSS.sample_Pnx: chain c = (point, sample) from x[point] with key split(c),
+// n frozen transitions with the shared (loc, factor), the transition's
+// stream position the step index
+__global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
+  extern __shared__ float lds_big[];
+  const int d = p.d;
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb0 = lds_big + (size_t)wv * 2 * kColBlk * d;
+  float* wb1 = wb0 + kColBlk * d;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t C = p.n_points * p.n_samples;
+  float dl[kNS], inv[kNS];
+  static_for<kNS>([&](auto K) {
+    const int r = 64 * K + lane;
+    const bool act = r < d;
+    dl[K] = act ? p.scale[col_off(d, act ? r : 0)] : 0.0f;
+    inv[K] = (amh_isfinite(dl[K]) && dl[K] != 0.0f) ? 1.0f / dl[K] : 0.0f;
+  });
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < C; c += nw) {
+    const int64_t pt = c / p.n_samples;
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, p.key0, p.key1);
+    float x[kNS], mu[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      x[K] = act ? p.x[pt * d + r] : 0.0f;
+      mu[K] = act ? p.loc[r] : 0.0f;
+    });
+    float pe = 0.0f, asc = 0.0f;
+    for (int32_t t = 0; t < p.n; ++t)
+      asss_big_chain<false>(p.scale, nullptr, dl, inv, x, mu, pe, asc, t, kk.v[0], kk.v[1], d, P, p.eps, 0, 0.0f,
+                            p.model, wb0, wb1, lane);
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) p.out[c * d + r] = x[K];
+    });
+  }
+}
+
 // ------------------------------------------------------------- launchers ----
 bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256 && d % 32 == 0; }
 // pooled mode: the MFMA path also takes d = 64 (every per-chain product is a
@@ -568,6 +969,14 @@ hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
   } else {
     hipLaunchKernelGGL(big_step_kernel<false>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   }
+  return hipGetLastError();
+}
+hipError_t run_asss_big_step(const StepParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(asss_big_step_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  return hipGetLastError();
+}
+hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(asss_big_pnx_kernel, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_potential(const PotParams& p, hipStream_t s) {

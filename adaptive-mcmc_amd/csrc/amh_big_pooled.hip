@@ -130,6 +130,8 @@ hipError_t diag_f64_stamps_copy(void* host) {
 #endif
 __device__ __forceinline__ f32x4 ld4(const float* a) { return *(const f32x4*)a; }
 
+// MULTI = false: one step (sync_every = 1), the step loop compiled away.
+template <bool MULTI>
 __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParams p, int64_t n_chunks) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int d = kF;
@@ -315,7 +317,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   // chunk's sums run over (sub-chunk, step, chain) -- orc_pooled_stats64_k.
   // Step 0's noise may come from the buffer the update launch drew ahead;
   // the others are drawn here (noise_phase).
-  const int32_t K = p.k_steps;
+  const int32_t K = MULTI ? p.k_steps : 1;
   int64_t q = 0;  // steps of this block so far (tile parity)
   for (int64_t t = 0; t < nmine; ++t) {
     const int64_t c0 = sub_c0(t);
@@ -2037,7 +2039,10 @@ hipError_t run_pooled_big_stats(const PooledStatsParams& p, float* xprop, float*
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
     const int64_t grid = nch < 2 * (int64_t)cus ? nch : 2 * (int64_t)cus;  // persistent, two per CU
-    hipLaunchKernelGGL(pooled_fused64_kernel, dim3((unsigned)grid), dim3(256), fused64_lds_bytes(), s, p, nch);
+    if (p.k_steps > 1)
+      hipLaunchKernelGGL(pooled_fused64_kernel<true>, dim3((unsigned)grid), dim3(256), fused64_lds_bytes(), s, p, nch);
+    else
+      hipLaunchKernelGGL(pooled_fused64_kernel<false>, dim3((unsigned)grid), dim3(256), fused64_lds_bytes(), s, p, nch);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     (void)V;

@@ -471,7 +471,9 @@ int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const 
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_asss_step: no model bound");
   if (!asss_state_ok(in) || !asss_state_ok(out) || num_chains < 1 || n_steps < 0)
     return fail(h, AMH_EINVAL, "amh_asss_step: bad arguments");
-  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64");
+  const bool big = amh::big_model(h->model_id, h->cfg.dim);
+  if (h->cfg.dim > 64 && !big)
+    return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64, or a dense Gaussian with d % 32 == 0 up to 256");
   if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_asss_step: thinning must be >= 1");
   if (n_steps == 0) return AMH_OK;
   hipError_t e = hipSetDevice(h->device);
@@ -493,6 +495,23 @@ int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const 
   p.gamma_tab = h->gamma_tab;
   p.gamma_tab_n = amh::kGammaTab;
   p.model = h->model;
+  if (big) {
+    // large d: one launch per transition (the factor streamed four times),
+    // the first from `in`, the rest in place on `out`
+    const int64_t keep_stride = num_chains * (int64_t)h->cfg.dim;
+    for (int32_t t = 0; t < n_steps; ++t) {
+      amh::StepParams q = p;
+      if (t > 0) q.in = *out;
+      q.n_steps = 1;
+      const bool keep = (t + 1) % p.thinning == 0;
+      const int64_t k = (t + 1) / p.thinning - 1;
+      q.col_z = (keep && p.col_z) ? p.col_z + k * keep_stride : nullptr;
+      q.col_pe = (keep && p.col_pe) ? p.col_pe + k * num_chains : nullptr;
+      e = amh::run_asss_big_step(q, (hipStream_t)stream);
+      if (e != hipSuccess) return hip_fail(h, e, "amh_asss_step(large d)");
+    }
+    return AMH_OK;
+  }
   e = amh::run_asss_step(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_asss_step");
   return AMH_OK;
@@ -504,7 +523,9 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_asss_sample_pnx: no model bound");
   if (!key || !x || !loc || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
     return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: bad arguments");
-  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64");
+  const bool big = amh::big_model(h->model_id, h->cfg.dim);
+  if (h->cfg.dim > 64 && !big)
+    return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64, or a dense Gaussian with d % 32 == 0 up to 256");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx/hipSetDevice");
   amh::AsssPnxParams p{};
@@ -520,7 +541,7 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
   p.key1 = key[1];
   p.out = out;
   p.model = h->model;
-  e = amh::run_asss_pnx(h->model_id, p, (hipStream_t)stream);
+  e = big ? amh::run_asss_big_pnx(p, (hipStream_t)stream) : amh::run_asss_pnx(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx");
   return AMH_OK;
 }

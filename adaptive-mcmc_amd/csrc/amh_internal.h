@@ -221,6 +221,10 @@ hipError_t run_big_propose(const BigParams& p, hipStream_t s);
 // next: also form the next transition's proposal and solves (multi-step launches)
 hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next = false);
 hipError_t run_big_potential(const PotParams& p, hipStream_t s);
+// ASSS for the large-d Gaussian (big_model): one transition per launch; the
+// frozen kernel of sample_Pnx
+hipError_t run_asss_big_step(const StepParams& p, hipStream_t s);
+hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s);
 
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain
 // batched potential, then the step kernel reading U(z') (amh_split.hip)

@@ -1563,9 +1563,261 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
 
 /* n_steps ASSS transitions of chains [0, C) in place (one kernel launch);
  * collect_z [n_steps][C][d] / collect_pe [n_steps][C] nullable. */
+/* ASSS for large dimensions (asss.py:192-269; 64 < d <= 256, d % 32 == 0,
+ * the dense Gaussian; round 5).  Kernel mirror of amh_asss_big.hip: one wave
+ * per chain, lane l owns rows 64 s + l, the factor streamed column by column
+ * (the large-d ARWMH path's layout), four passes over it per transition:
+ *   A  y = S^-1 (x - mu), S = (L + eps I) sqrt(d) (asss.py:214, :33-45):
+ *      column j: y_j = b_j / D_j, g = y_j e_j, b_r = fmaf(-U_rj, g, b_r) (r > j)
+ *   B  S z and S v in column order, one accumulator per row, the diagonal
+ *      (U_rr = 1) at column r, then + eps sqrt(d) z_r (resp. v_r)
+ *   the potential along the slice circle: with a = S z, b = S v, g = mu - m,
+ *      D(th) = (a c + b s) / om + g and Y(th) = (Pa c + Pb s) / om + Pg, where
+ *      Pa, Pb, Pg are fmaf chains over k of P[k][r] (once per transition);
+ *      U(th) = 0.5 big_sum(D Y) + c0 -- each shrink step is O(d)
+ *   C  w = U^-1 delta (s_r = fmaf(U_rj, w_j, s_r), w_j = delta_j - s_j)
+ *   D  the rank-one update as the large-d ARWMH step pass with a_j = q_j -
+ *      dl_j, b_j = c_j q_j (no step size), sdiff = sqrt(big_sum(row sums)).
+ * Draws as the d <= 64 kernel (Philox(r, i, 0, TAG_ASSS)).  as_change =
+ * ||mu' - mu|| + ||L' - L||_F (asss.py:259-267). */
+static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t* i_, float* z, float* pe,
+                           float* mu, float* L, float* asc, const uint32_t* keys, int adapt,
+                           const float* Lshared, const float* mushared) {
+  const int d = cfg->d;
+  const int64_t P = packed_size(d);
+  const float* Lc = adapt ? L + c * P : Lshared;
+  const float* mc = adapt ? mu + c * d : mushared;
+  const float* m = cfg->data;
+  const float* Pm = cfg->data + d;
+  const float c0 = cfg->data[d + d * d];
+  for (int r = 0; r < d; ++r) {
+    s->dl[r] = Lc[col_off(d, r)];
+    s->inv[r] = (amh_isfinite(s->dl[r]) && s->dl[r] != 0.0f) ? 1.0f / s->dl[r] : 0.0f;
+    s->z[r] = z[c * d + r];
+    s->mu[r] = mc[r];
+  }
+  for (int j = 0; j < d; ++j)
+    for (int r = j + 1; r < d; ++r) s->U[r][j] = Lc[col_off(d, j) + (r - j)] * s->inv[j];
+  const uint32_t it = (uint32_t)i_[c];
+  const uint32_t k0 = keys[2 * c], k1 = keys[2 * c + 1];
+  const float sd = sqrtf((float)d);
+  const float epsd = cfg->eps * sd;
+  const float fd = (float)d;
+  /* draws (asss.py:207, 219, 225, 60) */
+  float v[ORC_BIG];
+  for (int r = 0; r < d; ++r) v[r] = amh_normal_from_bits(amh_philox4x32_10((uint32_t)r, it, 0u, AMH_TAG_ASSS, k0, k1).v[0]);
+  const amh_u32x4 o0 = amh_philox4x32_10(0u, it, 0u, AMH_TAG_ASSS, k0, k1);
+  float vd = amh_normal_from_bits(o0.v[1]);
+  const float ut = amh_unif01_from_bits(o0.v[2]);
+  const float th0 = 6.28318548f * amh_unif01_from_bits(o0.v[3]);
+  /* pass A */
+  float e[ORC_BIG], invD[ORC_BIG], b[ORC_BIG], y[ORC_BIG], t[ORC_BIG];
+  for (int r = 0; r < d; ++r) {
+    e[r] = s->dl[r] * sd;
+    invD[r] = 1.0f / ((s->dl[r] + cfg->eps) * sd);
+    b[r] = s->z[r] - s->mu[r];
+  }
+  for (int j = 0; j < d; ++j) {
+    const float yl = b[j] * invD[j];
+    y[j] = yl;
+    const float g = yl * e[j];
+    for (int r = j + 1; r < d; ++r) b[r] = fmaf(-s->U[r][j], g, b[r]);
+  }
+  for (int r = 0; r < d; ++r) t[r] = y[r] * y[r];
+  const float ns = big_sum(t, d);
+  const float den = ns + 1.0f;
+  float zr[ORC_BIG];
+  for (int r = 0; r < d; ++r) zr[r] = (2.0f * y[r]) / den;
+  const float zd = (ns - 1.0f) / den;
+  /* tangent v (the d <= 64 kernel's rule for |v| = 0) */
+  for (int r = 0; r < d; ++r) t[r] = v[r] * zr[r];
+  const float dot = big_sum(t, d) + (vd * zd);
+  for (int r = 0; r < d; ++r) v[r] = fmaf(-dot, zr[r], v[r]);
+  vd = fmaf(-dot, zd, vd);
+  for (int r = 0; r < d; ++r) t[r] = v[r] * v[r];
+  float nv = sqrtf(big_sum(t, d) + (vd * vd));
+  if (orc_test_zero_tangent) nv = 0.0f;
+  const int degen = !(nv > 0.0f);
+  for (int r = 0; r < d; ++r) v[r] = degen ? 0.0f : v[r] / nv;
+  vd = degen ? 0.0f : vd / nv;
+  /* pass B */
+  float a[ORC_BIG], bb[ORC_BIG], hz[ORC_BIG], hv[ORC_BIG];
+  for (int r = 0; r < d; ++r) {
+    hz[r] = e[r] * zr[r];
+    hv[r] = e[r] * v[r];
+    a[r] = bb[r] = 0.0f;
+  }
+  for (int j = 0; j < d; ++j) {
+    a[j] = fmaf(1.0f, hz[j], a[j]);
+    bb[j] = fmaf(1.0f, hv[j], bb[j]);
+    for (int r = j + 1; r < d; ++r) {
+      a[r] = fmaf(s->U[r][j], hz[j], a[r]);
+      bb[r] = fmaf(s->U[r][j], hv[j], bb[r]);
+    }
+  }
+  float Sz[ORC_BIG], Sv[ORC_BIG], gm[ORC_BIG], Pa[ORC_BIG], Pb[ORC_BIG], Pg[ORC_BIG];
+  for (int r = 0; r < d; ++r) {
+    Sz[r] = a[r] + epsd * zr[r];
+    Sv[r] = bb[r] + epsd * v[r];
+    gm[r] = s->mu[r] - m[r];
+    Pa[r] = Pb[r] = Pg[r] = 0.0f;
+  }
+  for (int k = 0; k < d; ++k)
+    for (int r = 0; r < d; ++r) {
+      const float pk = Pm[k * d + r];
+      Pa[r] = fmaf(pk, Sz[k], Pa[r]);
+      Pb[r] = fmaf(pk, Sv[k], Pb[r]);
+      Pg[r] = fmaf(pk, gm[k], Pg[r]);
+    }
+  /* the point at angle (cs, sn): potential and x */
+  float xt[ORC_BIG], x0[ORC_BIG];
+#define ASSS_BIG_EVAL(CS, SN, XOUT, OM, UOUT)                                   \
+  do {                                                                         \
+    OM = 1.0f - ((zd * (CS)) + (vd * (SN)));                                   \
+    for (int r = 0; r < d; ++r) {                                              \
+      const float num = (Sz[r] * (CS)) + (Sv[r] * (SN));                       \
+      const float Dr = (num / OM) + gm[r];                                     \
+      const float Yr = (((Pa[r] * (CS)) + (Pb[r] * (SN))) / OM) + Pg[r];      \
+      t[r] = Dr * Yr;                                                          \
+      XOUT[r] = (num / OM) + s->mu[r];                                         \
+    }                                                                          \
+    UOUT = (0.5f * big_sum(t, d)) + c0;                                        \
+  } while (0)
+  float om0, U0;
+  ASSS_BIG_EVAL(1.0f, 0.0f, x0, om0, U0);
+  const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
+  float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
+  int iter = 0;
+  float ux;
+  int cont;
+  {
+    float sn, cs, om;
+    amh_sincosf(th, &sn, &cs);
+    ASSS_BIG_EVAL(cs, sn, xt, om, ux);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    cont = !degen && ((pt > tpe) || (om < cfg->eps));
+  }
+  while (cont) {
+    if (th < 0.0f) thmin = th;
+    if (th >= 0.0f) thmax = th;
+    const amh_u32x4 o = amh_philox4x32_10((uint32_t)iter, it, 1u, AMH_TAG_ASSS, k0, k1);
+    th = thmin + (thmax - thmin) * amh_unif01_from_bits(o.v[0]);
+    float sn, cs, om;
+    amh_sincosf(th, &sn, &cs);
+    ASSS_BIG_EVAL(cs, sn, xt, om, ux);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    iter += 1;
+    cont = (iter < 50) && ((pt > tpe) || (om < cfg->eps));
+  }
+#undef ASSS_BIG_EVAL
+  const int capped = degen || iter >= 50;
+  float xn[ORC_BIG];
+  for (int r = 0; r < d; ++r) xn[r] = capped ? x0[r] : xt[r];
+  float pen = capped ? U0 : ux;
+  if (amh_isnan(pen)) pen = INFINITY;
+  if (!adapt) {
+    for (int r = 0; r < d; ++r) z[c * d + r] = xn[r];
+    pe[c] = pen;
+    return;
+  }
+  /* adaptation (asss.py:246-267) */
+  const int32_t itr = (int32_t)it + 1;
+  const int32_t n = ((int32_t)it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
+  const float gamma = amh_lr_gamma(n, cfg->lr_decay);
+  float delta[ORC_BIG], mun[ORC_BIG], Dg[ORC_BIG], one[ORC_BIG], ws[ORC_BIG], sw[ORC_BIG], gw2[ORC_BIG];
+  float bsc[ORC_BIG], cc[ORC_BIG], qq[ORC_BIG], sacc[ORC_BIG];
+  const float sq = sqrtf(1.0f - gamma);
+  for (int r = 0; r < d; ++r) {
+    delta[r] = xn[r] - s->mu[r];
+    mun[r] = s->mu[r] + gamma * delta[r];
+    const float dm = mun[r] - s->mu[r];
+    t[r] = dm * dm;
+    const float ajj = sq * s->dl[r];
+    Dg[r] = ajj * ajj;
+    one[r] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : NAN;
+    sw[r] = 0.0f;
+  }
+  const float locd = sqrtf(big_sum(t, d));
+  /* pass C */
+  for (int j = 0; j < d; ++j) {
+    ws[j] = delta[j] - sw[j];
+    for (int r = j + 1; r < d; ++r) sw[r] = fmaf(s->U[r][j], ws[j], sw[r]);
+  }
+  for (int r = 0; r < d; ++r) {
+    gw2[r] = gamma * (ws[r] * ws[r]);
+    t[r] = gw2[r] / Dg[r];
+  }
+  big_excl_scan(t, bsc, d);
+  int revert = 0;
+  for (int r = 0; r < d; ++r) {
+    const float bq = 1.0f + bsc[r];
+    const float g2 = (bq * Dg[r]) + gw2[r];
+    const float dn = g2 / bq;
+    cc[r] = (gamma * ws[r]) / g2;
+    qq[r] = sqrtf(dn);
+    revert |= amh_isnan(fmaf(cc[r], 0.0f, one[r]) * qq[r]);
+  }
+  float sdiff = 0.0f;
+  if (!revert) {
+    /* pass D */
+    float* Lw = L + c * P;
+    float ac[ORC_BIG], bc[ORC_BIG], sv[ORC_BIG];
+    for (int r = 0; r < d; ++r) {
+      ac[r] = qq[r] - s->dl[r];
+      bc[r] = cc[r] * qq[r];
+      sv[r] = 0.0f;
+      sacc[r] = 0.0f;
+    }
+    for (int j = 0; j < d; ++j) {
+      {
+        const float tt = fmaf(1.0f, ac[j], bc[j] * 0.0f);
+        sacc[j] = fmaf(tt, tt, sacc[j]);
+        Lw[col_off(d, j)] = 1.0f * qq[j];
+      }
+      for (int r = j + 1; r < d; ++r) {
+        const float uo = s->U[r][j];
+        sv[r] = fmaf(uo, ws[j], sv[r]);
+        const float w = delta[r] - sv[r];
+        const float un = fmaf(cc[j], w, uo);
+        const float tt = fmaf(uo, ac[j], bc[j] * w);
+        sacc[r] = fmaf(tt, tt, sacc[r]);
+        Lw[col_off(d, j) + (r - j)] = un * qq[j];
+      }
+    }
+    sdiff = sqrtf(big_sum(sacc, d));
+  }
+  asc[c] = locd + sdiff;
+  for (int r = 0; r < d; ++r) {
+    z[c * d + r] = xn[r];
+    mu[c * d + r] = mun[r];
+  }
+  i_[c] = itr;
+  pe[c] = pen;
+}
+
+static int orc_asss_big(const orc_cfg* cfg) {
+  return cfg->model_id == ORC_GAUSSIAN && cfg->d > ORC_DMAX && cfg->d <= ORC_BIG && cfg->d % 32 == 0;
+}
+
 void orc_asss_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe, float* mu,
                    float* L, float* asc, const uint32_t* keys, float* collect_z, float* collect_pe) {
   const int d = cfg->d;
+  if (orc_asss_big(cfg)) {
+#pragma omp parallel for schedule(dynamic, 1)
+    for (int64_t c = 0; c < C; ++c) {
+      bigchain_t* s = (bigchain_t*)malloc(sizeof(bigchain_t));
+      for (int32_t t = 0; t < n_steps; ++t) {
+        asss_step_big1(cfg, s, c, i_, z, pe, mu, L, asc, keys, 1, NULL, NULL);
+        if (collect_z)
+          for (int r = 0; r < d; ++r) collect_z[((int64_t)t * C + c) * d + r] = z[c * d + r];
+        if (collect_pe) collect_pe[(int64_t)t * C + c] = pe[c];
+      }
+      free(s);
+    }
+    return;
+  }
   if (d > ORC_DMAX) return;
 #pragma omp parallel for schedule(dynamic, 16)
   for (int64_t c = 0; c < C; ++c) {
@@ -1612,6 +1864,25 @@ void orc_asss_sample_pnx(const orc_cfg* cfg, const uint32_t* key, const float* x
                          int64_t n_samples, const float* loc, const float* Lpacked, int32_t n, float* out) {
   const int d = cfg->d;
   const int64_t C = n_points * n_samples;
+  if (orc_asss_big(cfg)) { /* the frozen large-d transition (asss_step_big1, adapt = 0) */
+#pragma omp parallel for schedule(dynamic, 4)
+    for (int64_t c = 0; c < C; ++c) {
+      bigchain_t* s = (bigchain_t*)malloc(sizeof(bigchain_t));
+      const int64_t p = c / n_samples;
+      const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, key[0],
+                                             key[1]);
+      const uint32_t k2[2] = {kk.v[0], kk.v[1]};
+      float zc[ORC_BIG], pe1 = 0.0f;
+      for (int r = 0; r < d; ++r) zc[r] = x[p * d + r];
+      for (int32_t t = 0; t < n; ++t) {
+        int32_t i1 = t;
+        asss_step_big1(cfg, s, 0, &i1, zc, &pe1, NULL, NULL, NULL, k2, 0, Lpacked, loc);
+      }
+      for (int r = 0; r < d; ++r) out[c * d + r] = zc[r];
+      free(s);
+    }
+    return;
+  }
 #pragma omp parallel for schedule(dynamic, 64)
   for (int64_t c = 0; c < C; ++c) {
     chain_t* s = (chain_t*)malloc(sizeof(chain_t));

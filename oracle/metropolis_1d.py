@@ -126,7 +126,7 @@ def exact_ratios(f, x, sP: float, sQ: float):
         y, K, r = quadrature(x, s)
         fy, fx = f(y), f(x)
         m1, m2 = expectations(fy, fx, K, r)
-        out.append((m1, m2 - m1 * m1))
+        out.append((m1, np.maximum(m2 - m1 * m1, 0.0)))  # (rounding can leave -1e-17)
     d = out[0][0] - out[1][0]
     h = np.abs(np.diff(x))
     return np.abs(np.diff(d)) / h, out[0][1], out[1][1]

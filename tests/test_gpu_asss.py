@@ -50,7 +50,9 @@ def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
 @pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 600), ("gaussian", 5, 517), ("gaussian", 16, 300),
                                       ("gaussian", 33, 130), ("eight_schools", None, 400), ("kidiq", None, 257),
                                       ("diamonds", None, 66), ("diamonds_ss", None, 300), ("mixture", 1, 1000),
-                                      ("mixture", 3, 200)])
+                                      ("mixture", 3, 200),
+                                      # large d (amh_big.hip asss_big_step_kernel, round 5)
+                                      ("gaussian", 96, 130), ("gaussian", 128, 100), ("gaussian", 256, 70)])
 def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
     """ASSS.sample (one launch per step, out of place) vs oracle, 25 steps."""
     k, st, om, ost = _init(kind, C, orc, d=d, num_warmup=8)
@@ -62,7 +64,8 @@ def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
         assert_bitequal(st, ost, f"{kind} step {t}")
 
 
-@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("eight_schools", None, 700), ("diamonds", None, 40)])
+@pytest.mark.parametrize("kind,d,C", [("gaussian", 64, 1000), ("eight_schools", None, 700), ("diamonds", None, 40),
+                                      ("gaussian", 128, 60), ("gaussian", 256, 33)])
 def test_asss_fused_and_collect_bitexact(kind, d, C, gpu, orc):
     """ASSS.run (n steps per launch, z / pe collected with thinning) and the
     in-place ASSS.sample_ vs the oracle's launch-for-launch mirror."""
@@ -92,6 +95,47 @@ def test_asss_sample_pnx_bitexact(gpu, orc):
     ref = orc.asss_sample_pnx(om, PRNGKey(9), x.cpu().numpy(), loc.cpu().numpy(), scale.cpu().numpy(), 4, 37)
     assert out.shape == (5, 37, om.d)
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("d", [128, 256])
+def test_asss_sample_pnx_large_d_bitexact(d, gpu, orc):
+    """The large-d frozen kernel (asss_big_pnx_kernel) vs orc_asss_sample_pnx."""
+    from kernels_amd import PRNGKey
+    k, st, om, ost = _init("gaussian", 16, orc, d=d)
+    k.sample_(st, 20)
+    a = st.adapt_state
+    loc, scale = a.loc[3].clone(), a.scale[3].clone()
+    x = st.z[:3].clone()
+    out = k.sample_Pnx(PRNGKey(9), x, (loc, scale), n=3, n_samples=11)
+    ref = orc.asss_sample_pnx(om, PRNGKey(9), x.cpu().numpy(), loc.cpu().numpy(), scale.cpu().numpy(), 3, 11)
+    assert out.shape == (3, 11, d)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+
+
+def test_asss_large_d_samples_target(gpu):
+    """d = 128 correlated Gaussian, 512 chains, 3000 ASSS transitions: the
+    draws' per-coordinate variance matches the target's (the median ratio;
+    the chains' own adapted L L^T lags at about 0.2 x Sigma here as at
+    d = 64 -- the reference's recurrence with delta from the old mean,
+    asss.py:251-255, reproduced by the oracle), mean 0, as_change shrinking."""
+    import posteriors as P
+    from kernels_amd import ASSS, PRNGKey
+    g = P.correlated_gaussian(128)
+    k = ASSS(potential_fn=g, num_chains=512)
+    z0 = (torch.rand(512, 128, device="cuda") * 4 - 2).contiguous()
+    st = k.init(PRNGKey(5), 0, z0, (), {})
+    k.sample_(st, 200)
+    torch.cuda.synchronize()
+    asc0 = float(st.as_change.mean())
+    k.sample_(st, 2800)
+    torch.cuda.synchronize()
+    cov = np.linalg.inv(np.asarray(g.precision, np.float64))
+    z = st.z.double().cpu().numpy()
+    assert np.all(np.isfinite(z))
+    ratio = np.median(z.var(0) / np.diag(cov))
+    assert 0.7 < ratio < 1.25, ratio
+    assert abs(float(z.mean())) < 0.1
+    assert float(st.as_change.mean()) < asc0
 
 
 def test_asss_eight_schools_posterior(gpu):

@@ -82,7 +82,7 @@ def train(seed, x, mode, steps=1000, lr=0.1, rad=5, n_samp=1000):
 def analyse(model, x, rng, n_eval=10 ** 6, n_mc=20000):
     f = lambda t: model(torch.tensor(t).reshape(-1, 1)).detach().numpy()  # noqa: E731
     r, vP, vQ = M.exact_ratios(f, x, SP, SQ)
-    v = (vP + vQ) / n_eval
+    v = np.maximum(vP + vQ, 0.0) / n_eval
     h = np.abs(np.diff(x))
     # the estimator: d_j + e_j per point, e_j ~ N(0, v_j) independent
     y, K, rr = M.quadrature(x, SP)
@@ -106,7 +106,7 @@ def main():
     ap.add_argument("--modes", default="exact,mc")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
-    torch.set_num_threads(max(1, min(8, os.cpu_count() or 1)))
+    torch.set_num_threads(int(os.environ.get("CELL101_THREADS", max(1, min(8, os.cpu_count() or 1)))))
     lines = []
 
     def say(s):
