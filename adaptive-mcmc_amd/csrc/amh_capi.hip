@@ -386,6 +386,7 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
     q.n_steps = 1;
     q.thinning = 1;
     q.ext_pe = peprop;
+    q.ext_z = xprop;
     for (int32_t t = 0; t < n_steps; ++t) {
       q.in = (t == 0) ? *in : *out;
       const bool keep = ((t + 1) % p.thinning) == 0;

@@ -290,6 +290,13 @@ template <class T>
 __device__ __forceinline__ void lds_wait(T& a, T& b, T& c, T& d) {
   asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d));
 }
+template <int N, class T>
+__device__ __forceinline__ void lds_wait_n(T (&v)[N]) {
+  static_assert(N == 1 || N == 2 || N == 4, "lds_wait_n: 1, 2 or 4 values");
+  if constexpr (N == 1) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]));
+  if constexpr (N == 2) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v[0]), "+v"(v[1]));
+  if constexpr (N == 4) lds_wait(v[0], v[1], v[2], v[3]);
+}
 
 // ------------------------------------------------------------------ models --
 // Every model: static potential(x_r, r, d, args, lds) -> U (same value in all

@@ -39,6 +39,7 @@ struct StepParams {
   int32_t gamma_tab_n;
   ModelArgs model;
   const float* ext_pe;     // split path: U(z') per chain from the batched potential (n_steps == 1)
+  const float* ext_z;      // split path: the proposals z' [C][d] that U(z') was evaluated at
   float* xprop_next;       // split path: the NEXT transition's proposal [C][d] (or null), formed as
                            // the propose pass would form it from the stored state
 };

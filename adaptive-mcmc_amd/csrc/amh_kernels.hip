@@ -168,9 +168,22 @@ template <int G, template <int> class M>
 __host__ __device__ __forceinline__ size_t tickets_off(const ModelArgs& m, int d) {
   return step_wbuf_off<G, M>(m, d) + (size_t)(kBlockStep / 64) * wbuf_floats(Geo<G>::CPW, d);
 }
+// G = 32: per-wave broadcast scratch (64 lanes x 4 floats) after the ticket --
+// the column sweeps read a column's four per-column scalars with one
+// ds_read_b128 instead of four DPP + permlane16 broadcasts (three
+// instructions each at this width)
+template <int G, template <int> class M>
+__host__ __device__ __forceinline__ size_t bcast_off(const ModelArgs& m, int d) {
+  return (tickets_off<G, M>(m, d) + 4 + 3) & ~(size_t)3;
+}
+constexpr int kBcastFloats = 64 * 4;
 template <int G, template <int> class M>
 __host__ __device__ __forceinline__ size_t step_lds_bytes(const ModelArgs& m, int d) {
+  if (G == 32) return (bcast_off<G, M>(m, d) + (size_t)(kBlockStep / 64) * kBcastFloats) * sizeof(float);
   return (tickets_off<G, M>(m, d) + 4) * sizeof(float);
+}
+__device__ __forceinline__ void lds_st4(uint32_t a, f32x4 v) {
+  asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
 // DFIX > 0: d fixed at compile time below the group width (the diamonds
@@ -199,6 +212,20 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   const float* wm = wz + wbuf_zd(CPW, d);
   const float* wsc = wm + wbuf_zd(CPW, d);
   const uint32_t oob = kOOB;
+#ifndef AMH_LDS_S2
+#define AMH_LDS_S2 1
+#endif
+#ifndef AMH_LDS_SP
+#define AMH_LDS_SP 1
+#endif
+#ifndef AMH_LDS_NB
+#define AMH_LDS_NB 4
+#endif
+  constexpr bool kLdsS2 = G == 32 && DFIX > 0 && AMH_LDS_S2;
+  constexpr bool kLdsSP = G == 32 && DFIX > 0 && !kExt && AMH_LDS_SP;  // (ExtPotM: spills)
+  constexpr int NB = AMH_LDS_NB;
+  [[maybe_unused]] const uint32_t bs_a =
+      lds_addr(lds + bcast_off<G, M>(p.model, d) + (size_t)wave_in_block * kBcastFloats);
 
   // Registers carry one chain group at a time.  Iteration k: wait for the
   // DMA of item k, write item k-1 back (its registers are still live), read
@@ -207,6 +234,16 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   float U[DMAX];
   float dl = 0.0f, z = 0.0f, mu = 0.0f, pe = 0.0f, macc = 0.0f, lam = 0.0f, asc = 0.0f;
   [[maybe_unused]] float pe_ext = 0.0f;  // split path: U(z') computed outside
+  // split path: the proposal U(z') was evaluated at, read from the split
+  // buffer (loaded for the next item while this one computes) instead of
+  // formed again -- the same bits (the propose pass / the previous step
+  // pass made it from this state), one column sweep and the normals fewer
+  [[maybe_unused]] float zp_nx = 0.0f, zp_cur = 0.0f;
+  auto load_zp = [&](int64_t it_item, int ln) {
+    const int rq = ln & (G - 1);
+    const int64_t ch = it_item * CPW + ln / G;
+    zp_nx = (rq < d && ch < C) ? p.ext_z[ch * d + rq] : 0.0f;
+  };
   int32_t it = 0, nacc = 0, acc0 = 0;
   uint32_t k0 = 0, k1 = 0;
   bool updated = false;
@@ -298,7 +335,10 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   int64_t item = ticket();
   int64_t nxt = item < blk_hi ? ticket() : blk_hi;
 
-  if (item < blk_hi) prefetch_item<G, kExt>(p, item * CPW, d, wb, lane_id());
+  if (item < blk_hi) {
+    prefetch_item<G, kExt>(p, item * CPW, d, wb, lane_id());
+    if constexpr (kExt) load_zp(item, lane_id());
+  }
   for (; item < blk_hi;) {
     // Every lane-dependent quantity is derived from an opaque copy of the lane
     // id inside the loop: otherwise the compiler hoists dozens of per-column
@@ -348,13 +388,17 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       asc = wsc[4 * CPW + g];
       k0 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g]);
       k1 = (uint32_t)__float_as_int(wsc[5 * CPW + 2 * g + 1]);
-      if constexpr (kExt) pe_ext = wsc[7 * CPW + g];
+      if constexpr (kExt) {
+        pe_ext = wsc[7 * CPW + g];
+        zp_cur = zp_nx;
+      }
     }
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): buffer consumed before it is refilled
     AMH_STAMP(2)
     int64_t nxt2 = blk_hi;
     if (nxt < blk_hi) {
       prefetch_item<G, kExt>(p, nxt * CPW, d, wb, lane);
+      if constexpr (kExt) load_zp(nxt, lane);
       nxt2 = ticket();
     }
     __builtin_amdgcn_s_setprio(0);
@@ -364,23 +408,30 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
-      float xi, u;
-      step_noise<G>(r, d, (uint32_t)it, k0, k1, xi, u);
-      xi = act ? xi : 0.0f;
-
-      // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
-      //      L xi = U (dl * xi)
+      float u, zp;
       const float el = amh_expf(lam);
-      const float eta = dl * xi;
-      // four interleaved partial sums (columns j mod 4): four independent
-      // FMA chains instead of one 64-long dependency chain
-      float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-      static_for<DMAX>([&](auto J) {
-        if (J < d) a4[J & 3] = fmaf(U[J], Gp::template bcast<J>(eta), a4[J & 3]);
-        column_fence<J, 16>();
-      });
-      const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
-      const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+      if constexpr (kExt) {
+        // split path (n_steps == 1): z' from the split buffer, u = U(W_d)
+        u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)it, k0, k1));
+        zp = act ? zp_cur : 0.0f;
+      } else {
+        float xi;
+        step_noise<G>(r, d, (uint32_t)it, k0, k1, xi, u);
+        xi = act ? xi : 0.0f;
+
+        // ---- proposal z' = z + (L e^lam + eps I) xi  (arwmh.py:166-167),
+        //      L xi = U (dl * xi)
+        const float eta = dl * xi;
+        // four interleaved partial sums (columns j mod 4): four independent
+        // FMA chains instead of one 64-long dependency chain
+        float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+        static_for<DMAX>([&](auto J) {
+          if (J < d) a4[J & 3] = fmaf(U[J], Gp::template bcast<J>(eta), a4[J & 3]);
+          column_fence<J, 16>();
+        });
+        const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
+        zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+      }
 
       // ---- potential, NaN -> +inf (arwmh.py:169-171)
       float pep;
@@ -455,21 +506,42 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         const float ac = (q * e1) - (dl * el);
         const float bc = (c * q) * e1;
         w = delta;
-        static_for<DMAX>([&](auto J) {
-          if (J < d) {
-            const float wj = Gp::template bcast<J>(ws);
-            const float cj = Gp::template bcast<J>(c);
-            const float aj = Gp::template bcast<J>(ac);
-            const float bj = Gp::template bcast<J>(bc);
-            const float uo = U[J];
-            w = fmaf(-wj, uo, w);
-            const float un = fmaf(cj, w, uo);
-            const float tt = fmaf(uo, aj, bj * w);
-            s4[J & 3] = fmaf(tt, tt, s4[J & 3]);
-            U[J] = un;
-          }
-          column_fence<J>();
-        });
+        auto col2 = [&](auto J, float wj, float cj, float aj, float bj) {
+          const float uo = U[J];
+          w = fmaf(-wj, uo, w);
+          const float un = fmaf(cj, w, uo);
+          const float tt = fmaf(uo, aj, bj * w);
+          s4[J & 3] = fmaf(tt, tt, s4[J & 3]);
+          U[J] = un;
+        };
+        if constexpr (kLdsS2) {
+          // the group's (ws, c, ac, bc) through the wave's LDS scratch, four
+          // columns per wait (asm reads: no vmcnt wait on the DMA prefetch)
+          lds_st4(bs_a + 16u * (uint32_t)lane, f32x4{ws, c, ac, bc});
+          const uint32_t ga = bs_a + 16u * (uint32_t)(g * G);
+          static_for<(DMAX + NB - 1) / NB>([&](auto B) {
+            f32x4 qv[NB];
+            static_for<NB>([&](auto Q) {
+              constexpr int j = NB * B + Q;
+              qv[Q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+              if (j < d) qv[Q] = lds_ld4<16 * j>(ga);
+            });
+            lds_wait_n<NB>(qv);
+            static_for<NB>([&](auto Q) {
+              constexpr int j = NB * B + Q;
+              if (j < d) col2(std::integral_constant<int, j>{}, qv[Q][0], qv[Q][1], qv[Q][2], qv[Q][3]);
+            });
+            column_fence<NB * B + NB - 1>();
+          });
+        } else {
+          static_for<DMAX>([&](auto J) {
+            if (J < d) {
+              col2(J, Gp::template bcast<J>(ws), Gp::template bcast<J>(c), Gp::template bcast<J>(ac),
+                   Gp::template bcast<J>(bc));
+            }
+            column_fence<J>();
+          });
+        }
         sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
         asc = sqrtf(Gp::sum(act ? sacc : 0.0f));
         dl = act ? q : 0.0f;
@@ -519,20 +591,41 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
         const float el = amh_expf(lam);
         const float eta = dl * xi;
         float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-        static_for<DMAX>([&](auto J) {
+        auto colp = [&](auto J, float dj, float ij, float ej) {
           constexpr int j = J;
-          if (j < d) {
-            // the broadcasts run with every lane of the group active (a
-            // broadcast under a lane-dependent branch would read an inactive
-            // source lane); then the load path's own masking
-            const float dj = Gp::template bcast<j>(dl);
-            const float ij = Gp::template bcast<j>(inv);
-            const float ej = Gp::template bcast<j>(eta);
-            const float un = set_one_at<G, j>(keep_above<G, j>((U[j] * dj) * ij, rr), rr);
-            a4[j & 3] = fmaf(any_upd ? un : U[j], ej, a4[j & 3]);
-          }
-          column_fence<j, 16>();
-        });
+          const float un = set_one_at<G, j>(keep_above<G, j>((U[j] * dj) * ij, rr), rr);
+          a4[j & 3] = fmaf(any_upd ? un : U[j], ej, a4[j & 3]);
+        };
+        if constexpr (kLdsSP) {
+          // (dl, 1 / dl, eta) through the LDS scratch, as sweep 2
+          lds_st4(bs_a + 16u * (uint32_t)lane, f32x4{dl, inv, eta, 0.0f});
+          const uint32_t ga = bs_a + 16u * (uint32_t)(g * G);
+          static_for<(DMAX + NB - 1) / NB>([&](auto B) {
+            f32x4 qv[NB];
+            static_for<NB>([&](auto Q) {
+              constexpr int j = NB * B + Q;
+              qv[Q] = f32x4{0.0f, 0.0f, 0.0f, 0.0f};
+              if (j < d) qv[Q] = lds_ld4<16 * j>(ga);
+            });
+            lds_wait_n<NB>(qv);
+            static_for<NB>([&](auto Q) {
+              constexpr int j = NB * B + Q;
+              if (j < d) colp(std::integral_constant<int, j>{}, qv[Q][0], qv[Q][1], qv[Q][2]);
+            });
+            column_fence<NB * B + NB - 1, 16>();
+          });
+        } else {
+          static_for<DMAX>([&](auto J) {
+            constexpr int j = J;
+            if (j < d) {
+              // the broadcasts run with every lane of the group active (a
+              // broadcast under a lane-dependent branch would read an inactive
+              // source lane); then the load path's own masking
+              colp(J, Gp::template bcast<j>(dl), Gp::template bcast<j>(inv), Gp::template bcast<j>(eta));
+            }
+            column_fence<j, 16>();
+          });
+        }
         const float acc = (a4[0] + a4[1]) + (a4[2] + a4[3]);
         const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
         if (chain_ok && act) p.xprop_next[chain * d + r] = zp;
