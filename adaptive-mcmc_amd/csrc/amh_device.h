@@ -86,6 +86,30 @@ struct Grp {
       return v;
     }
   }
+  // A value broadcast to many columns: at G = 32 one permlane16_swap per value
+  // (lo: rows 0 / 2 copied over rows 1 / 3; hi: rows 1 / 3 over rows 0 / 2),
+  // then each column is a single row_newbcast DPP of lo (J < 16) or hi --
+  // instead of a copy, a swap and a DPP per column as bcast<J> needs
+  struct Src {
+    int lo, hi;
+  };
+  static __device__ __forceinline__ Src src(float v) {
+    if constexpr (G == 32) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_int(v), __float_as_int(v), false, false);
+      return Src{(int)sw[0], (int)sw[1]};
+    } else {
+      return Src{__float_as_int(v), 0};
+    }
+  }
+  template <int J>
+  static __device__ __forceinline__ float bcast(const Src& s) {
+    if constexpr (G == 32) {
+      return __int_as_float(
+          __builtin_amdgcn_update_dpp(0, J < 16 ? s.lo : s.hi, dpp::kRowNewBcast0 + (J & 15), 0xF, 0xF, false));
+    } else {
+      return bcast<J>(__int_as_float(s.lo));
+    }
+  }
   template <int J>
   static __device__ __forceinline__ uint32_t bcast_u(uint32_t v) {
     return (uint32_t)__float_as_int(bcast<J>(__int_as_float((int)v)));

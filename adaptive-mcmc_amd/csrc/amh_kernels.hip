@@ -186,10 +186,25 @@ __device__ __forceinline__ void lds_st4(uint32_t a, f32x4 v) {
   asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
+#ifndef AMH_KARG_RELOAD
+#define AMH_KARG_RELOAD 1
+#endif
+typedef __attribute__((address_space(4))) const StepParams kconst_step_params;
+__device__ __forceinline__ const StepParams& reload_params(const StepParams& p) {
+#if AMH_KARG_RELOAD
+  kconst_step_params* pk = (kconst_step_params*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  return *(const StepParams*)pk;
+#else
+  return p;
+#endif
+}
+
 // DFIX > 0: d fixed at compile time below the group width (the diamonds
 // split path, d = 26 in groups of 32): column offsets become immediates.
 template <int DMAX, template <int> class M, bool EXACT, int DFIX = 0>
 __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
+  const StepParams& p_outer = p;
   constexpr int G = DMAX;
   constexpr int CPW = Geo<G>::CPW;
   constexpr bool kExt = is_external<M<G>>::value;
@@ -222,7 +237,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
 #define AMH_LDS_NB 4
 #endif
   constexpr bool kLdsS2 = G == 32 && DFIX > 0 && AMH_LDS_S2;
-  constexpr bool kLdsSP = G == 32 && DFIX > 0 && !kExt && AMH_LDS_SP;  // (ExtPotM: spills)
+  constexpr bool kLdsSP = G == 32 && DFIX > 0 && (!kExt || AMH_LDS_SP > 1) && AMH_LDS_SP;
   constexpr int NB = AMH_LDS_NB;
   [[maybe_unused]] const uint32_t bs_a =
       lds_addr(lds + bcast_off<G, M>(p.model, d) + (size_t)wave_in_block * kBcastFloats);
@@ -239,7 +254,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   // formed again -- the same bits (the propose pass / the previous step
   // pass made it from this state), one column sweep and the normals fewer
   [[maybe_unused]] float zp_nx = 0.0f, zp_cur = 0.0f;
-  auto load_zp = [&](int64_t it_item, int ln) {
+  auto load_zp = [&](const StepParams& p, int64_t it_item, int ln) {
     const int rq = ln & (G - 1);
     const int64_t ch = it_item * CPW + ln / G;
     zp_nx = (rq < d && ch < C) ? p.ext_z[ch * d + rq] : 0.0f;
@@ -251,7 +266,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   static_for<DMAX>([&](auto J) { U[J] = 0.0f; });
 
   // write the registers' chain group (item `it_item`) back to HBM
-  auto store_item = [&](int64_t it_item, int lane) {
+  auto store_item = [&](const StepParams& p, int64_t it_item, int lane) {
     const int r = lane & (G - 1);
     const int rr = r;
     const bool act = r < d;
@@ -269,11 +284,20 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     // (the branch is outside the column loop: a per-column select between a
     // load and a product made the compiler wait vmcnt(0) before every store)
     if (any_upd) {
+      const auto dls = Gp::src(dl);
       static_for<DMAX>([&](auto J) {
         constexpr int j = J;
         if (j < d) {
           const uint32_t so = (uint32_t)(col_off(d, j) - j) * 4u;
-          Lout.st(U[j] * Gp::template bcast<j>(dl), off_from<G, j>(vrow, oob, rr), so);
+          const float v = U[j] * Gp::template bcast<j>(dls);
+          if constexpr (EXACT || DFIX > 0) {
+            // d fixed: the column offset as the instruction's immediate (an
+            // SGPR offset costs an s_movk + hazard nop per column; kOOB + so
+            // stays out of range)
+            Lout.st(v, off_from<G, j>(vrow, oob, rr) + so, 0u);
+          } else {
+            Lout.st(v, off_from<G, j>(vrow, oob, rr), so);
+          }
         }
         column_fence<j>();
       });
@@ -337,7 +361,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
 
   if (item < blk_hi) {
     prefetch_item<G, kExt>(p, item * CPW, d, wb, lane_id());
-    if constexpr (kExt) load_zp(item, lane_id());
+    if constexpr (kExt) load_zp(p, item, lane_id());
   }
   for (; item < blk_hi;) {
     // Every lane-dependent quantity is derived from an opaque copy of the lane
@@ -345,6 +369,11 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     // addresses and masks out of this persistent loop and runs out of VGPRs.
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
+    // the launch parameters re-read from the kernarg segment each item
+    // (scalar loads through an opaque pointer): kept live across the loop,
+    // their ~60 SGPRs spilled to VGPR lanes and every item paid hundreds of
+    // v_readlane / v_writelane + hazard nops
+    const StepParams& p = reload_params(p_outer);
     const int r = lane & (G - 1);
     const int rr = r;
     const bool act = r < d;
@@ -356,7 +385,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this item's DMA has landed
     __builtin_amdgcn_s_setprio(3);  // hand-over phase first (as arwmh_step64_kernel): diamonds_ss +1.8 %
     AMH_STAMP(0)
-    if (prev >= 0) store_item(prev, lane);
+    if (prev >= 0) store_item(p, prev, lane);
     AMH_STAMP(1)
 
     // ---- state: LDS -> registers
@@ -368,12 +397,13 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
       const lds_float* Lg = (const lds_float*)(wL + g * P);
       dl = act ? Lg[col_off(d, r)] : 0.0f;
       const float inv = (amh_isfinite(dl) && dl != 0.0f) ? 1.0f / dl : 0.0f;
+      const auto invs = Gp::src(inv);
       static_for<DMAX>([&](auto J) {
         constexpr int j = J;
         U[j] = 0.0f;
         if (j < d) {
           const float x = Lrow[col_off(d, j) - j];  // garbage for r < j: masked below
-          U[j] = set_one_at<G, j>(keep_above<G, j>(x * Gp::template bcast<j>(inv), rr), rr);
+          U[j] = set_one_at<G, j>(keep_above<G, j>(x * Gp::template bcast<j>(invs), rr), rr);
         }
         column_fence<j>();
       });
@@ -398,7 +428,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     int64_t nxt2 = blk_hi;
     if (nxt < blk_hi) {
       prefetch_item<G, kExt>(p, nxt * CPW, d, wb, lane);
-      if constexpr (kExt) load_zp(nxt, lane);
+      if constexpr (kExt) load_zp(p, nxt, lane);
       nxt2 = ticket();
     }
     __builtin_amdgcn_s_setprio(0);
@@ -615,13 +645,14 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
             column_fence<NB * B + NB - 1, 16>();
           });
         } else {
+          const auto dls = Gp::src(dl), invs = Gp::src(inv), etas = Gp::src(eta);
           static_for<DMAX>([&](auto J) {
             constexpr int j = J;
             if (j < d) {
               // the broadcasts run with every lane of the group active (a
               // broadcast under a lane-dependent branch would read an inactive
               // source lane); then the load path's own masking
-              colp(J, Gp::template bcast<j>(dl), Gp::template bcast<j>(inv), Gp::template bcast<j>(eta));
+              colp(J, Gp::template bcast<j>(dls), Gp::template bcast<j>(invs), Gp::template bcast<j>(etas));
             }
             column_fence<j, 16>();
           });
@@ -641,7 +672,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   if (prev >= 0) {
     int lane = lane_id();
     asm volatile("" : "+v"(lane));
-    store_item(prev, lane);
+    store_item(p, prev, lane);
   }
   __builtin_amdgcn_s_waitcnt(0);
   AMH_STAMP(5)
