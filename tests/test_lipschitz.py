@@ -43,13 +43,16 @@ def test_contraction_and_kernel_distance_on_device(gpu):
     X = torch.linspace(-5, 5, 100).reshape(-1, 1)
     for n in (0, 1, 5):
         fn = lambda key, x, n_samples, n=n: k.sample_Pnx(key, x, adapt, n, n_samples)
+        # P^0 = I: the exact tau is 1 (sup over 1-Lipschitz f of a pair's
+        # |f(x) - f(y)| / |x - y|); the estimate is the trained f's own largest
+        # pair ratio, so it is trained until it gets there (10 Adam steps stop
+        # at 0.78 with the reference's fixed power-iteration start)
         tau, model, params = Lz.compute_wasserstein_contraction(fn, PRNGKey(0), X, n_train_batches=5,
-                                                                n_eval_batches=20, max_steps=10)
+                                                                n_eval_batches=20, max_steps=200 if n == 0 else 10)
         assert 0.0 < tau <= 1.15
         if n == 0:
-            # P^0 = I: tau is the trained f's own Lipschitz ratio after only 10
-            # Adam steps (0.78 with the reference's fixed power-iteration start)
-            assert tau > 0.7
+            print(f"tau(P^0) = {tau:.4f} (exact 1)")
+            assert 0.8 < tau <= 1.0 + 1e-4  # no noise at n = 0 (Pf = f); float32 ratio rounding
     fn = lambda key, x, n_samples: k.sample_Pnx(key, x, adapt, 1, n_samples)
     rho, _, _ = Lz.compute_kernel_distance_1d(fn, fn, PRNGKey(1), torch.linspace(-3, 3, 31), max_steps=10,
                                               n_eval_batches=10)
@@ -86,20 +89,30 @@ def test_kernel_distance_multid_on_device(gpu):
 @pytest.mark.gpu
 def test_kernel_distance_1d_notebook_cell101(gpu):
     """asumptions_check.ipynb cell 101: rho(P, Q) between the frozen 1-D
-    N(0, 1) kernels with scale 1 and 0.1, n = 1, x = linspace(-5, 5, 100) and
-    the notebook's rho_conf (1000 training steps, 1000 x 1000-sample
-    evaluation batches, ratio_rad 5).  The notebook prints 0.544187 from one
-    key, with its training unconverged (last clipped-gradient norm 0.44).
+    N(0, 1) kernels with scale 1 and 0.1 (+ eps 1e-6), n = 1, x =
+    linspace(-5, 5, 100) and the notebook's rho_conf (1000 training steps,
+    1000 x 1000-sample evaluation batches, ratio_rad 5).  The notebook prints
+    0.544187 from one key.
 
-    Known residual, stated rather than tuned away: with the
-    reference's fixed power-iteration start (round 4) the keys agree closely
-    -- 0.4825, 0.4514, 0.4490, 0.4781 on the r4f box, mean 0.465, sd 0.018,
-    final gradient norms 1e-3..1e-2 -- and sit 0.079 (4.5 sd) below the
-    notebook's value.  The restatement follows lipschitz.py:347-494 line by
-    line; the cause is not found (JAX/flax are not importable here).  What
-    this test pins is the build's own estimate: the trained f is 1-Lipschitz,
-    the keys agree, and the estimate stays where it was measured; the residual
-    to the notebook is printed and must not grow past 0.1."""
+    Pinned to exact answers (oracle/metropolis_1d.py, the kernel's CDF in
+    closed form; profiles/r5_cell101_*.txt, tools/cell101_exact.py):
+      * the value the estimator approaches with no noise is a property of
+        the TRAINED f: for each key the build's estimate must equal the exact
+        quadrature value of its own network's ratios, max_i |(P - Q) f(x_i+1)
+        - (P - Q) f(x_i)| / h, within the evaluation's Monte Carlo spread
+        (the max over 99 noisy ratios sits at most a few sd above it);
+      * no pair exceeds its Kantorovich-Rubinstein supremum over ALL
+        1-Lipschitz f (int |F_mu|; the largest is 0.9591 at x = 1.263), so
+        the notebook's 0.544 is reachable -- it is not bounded away;
+      * the keys land where the reference's own procedure lands: the float64
+        CPU restatement of lipschitz.py:396-491 (Monte Carlo training as the
+        notebook trains) gives exact rho 0.28..0.54 over 20 keys (mean 0.447,
+        sd 0.069; the notebook-style estimate 0.29..0.54), and 0.46..0.55
+        when trained on the exact objective.  The notebook's 0.544 is +1.4 sd
+        from that mean: a favourable key, not Monte Carlo evaluation bias
+        (<= 0.007 for every trained f) and not a short-fall of the build's
+        sampler or evaluation, which the first check pins."""
+    from oracle import metropolis_1d as M
     import posteriors as P
     from kernels_amd import ARWMH, PRNGKey
     g = P.gaussian(np.zeros(1), cov=np.eye(1))
@@ -109,23 +122,38 @@ def test_kernel_distance_1d_notebook_cell101(gpu):
     fp = lambda key, x, n_samples: k.sample_Pnx(key, x, s_p, 1, n_samples)
     fq = lambda key, x, n_samples: k.sample_Pnx(key, x, s_q, 1, n_samples)
     x = torch.linspace(-5, 5, 100)
+    x64 = x.double().numpy()
+    SP, SQ = 1.0 + 1e-6, 0.1 + 1e-6  # arwmh.py:166: L e^lam + eps
+    kr = M.kr_bound(x64, SP, SQ)
     grid = torch.linspace(-8, 8, 16001, device=gpu).reshape(-1, 1)
-    rhos = []
+    rows = []
     for seed in range(4):
         rho, model, _ = Lz.compute_kernel_distance_1d(fp, fq, PRNGKey(seed), x, sample_batch_size=1000,
                                                       n_train_batches=1, n_eval_batches=1000, max_steps=1000,
                                                       lr=0.1, ratio_rad=5)
+
+        def f(t, model=model):
+            with torch.no_grad():
+                tt = torch.as_tensor(np.asarray(t), dtype=torch.float32, device=gpu).reshape(-1, 1)
+                return model(tt).double().cpu().numpy()
+
         with torch.no_grad():
-            f = model(grid)
-            lip = float((f[1:] - f[:-1]).abs().max() / (grid[1, 0] - grid[0, 0]))
+            fg = model(grid)
+            lip = float((fg[1:] - fg[:-1]).abs().max() / (grid[1, 0] - grid[0, 0]))
         assert lip <= 1.01, (seed, lip)  # the spectral normalisation holds
-        rhos.append(rho)
-    m, sd = float(np.mean(rhos)), float(np.std(rhos, ddof=1))
-    print(f"cell 101 rho over keys 0..3: {np.round(rhos, 4).tolist()} mean {m:.4f} sd {sd:.4f} "
-          f"residual vs notebook {m - 0.544187:+.4f}")
-    assert sd < 0.05
-    assert 0.43 < m < 0.50
-    assert abs(m - 0.544187) < 0.1
+        r, vP, vQ = M.exact_ratios(f, x64, SP, SQ)
+        sd = M.mc_sd(vP, vQ, x64, 1000 * 1000)
+        i = int(r.argmax())
+        assert np.all(r <= max(lip, 1.0) * kr + 1e-6), seed
+        rows.append((rho, float(r[i]), float(sd[i])))
+        print(f"cell 101 key {seed}: estimate {rho:.4f}, exact rho of the trained f {r[i]:.4f} at x = {x64[i]:.3f} "
+              f"(ratio sd {sd[i]:.4f}), Lipschitz {lip:.4f}")
+        assert -4 * sd[i] - 1e-3 <= rho - r[i] <= 0.02, (seed, rho, r[i], sd[i])
+        assert 0.25 <= rho <= 0.56, (seed, rho)  # the restated procedure's range
+    m = float(np.mean([a for a, _, _ in rows]))
+    print(f"cell 101: mean over keys 0..3 {m:.4f}; KR supremum {kr.max():.4f}; notebook 0.544187 "
+          f"(restated procedure over 20 keys: 0.28..0.54, mean 0.447, sd 0.069)")
+    assert 0.544187 < kr.max()
 
 
 def test_power_iteration_start_is_fixed_like_fold_in():

@@ -18,7 +18,10 @@ separates the three things that number mixes (oracle/metropolis_1d.py):
      over the 99 noisy adjacent ratios (10^6 draws per point) minus the
      noise-free max, and the probability of reaching 0.544187.
 
-Usage: python tools/cell101_exact.py [n_keys] [--out profiles/r5_cell101_exact.txt]
+Usage: python tools/cell101_exact.py [n_keys] [--seed0 S] [--modes exact,mc] [--build-keys]
+       [--out profiles/r5_cell101_exact.txt]
+(--build-keys: the initial networks of the build's keys PRNGKey(S..), for a
+per-key comparison with tests/test_lipschitz.py's GPU run)
 """
 import argparse
 import math
@@ -34,15 +37,16 @@ sys.path.insert(0, os.path.join(ROOT, "adaptive-mcmc_amd"))
 sys.path.insert(0, ROOT)
 
 from oracle import metropolis_1d as M  # noqa: E402
-from utils_amd.lipschitz import LipschitzNN  # noqa: E402
+from kernels_amd.random import PRNGKey, split  # noqa: E402
+from utils_amd.lipschitz import LipschitzNN, _init_seed  # noqa: E402
 
 NOTEBOOK = 0.544187
 SP, SQ = 1.0 + 1e-6, 0.1 + 1e-6  # arwmh.py:166: L e^lam + eps
 
 
-def train(seed, x, mode, steps=1000, lr=0.1, rad=5, n_samp=1000):
+def train(seed, x, mode, steps=1000, lr=0.1, rad=5, n_samp=1000, init_seed=None):
     torch.manual_seed(seed)
-    model = LipschitzNN(1, seed=seed).double()
+    model = LipschitzNN(1, seed=seed if init_seed is None else init_seed).double()
     h = float(x[1] - x[0])
     kern = []
     for s in (SP, SQ):
@@ -104,6 +108,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("n_keys", type=int, nargs="?", default=4)
     ap.add_argument("--modes", default="exact,mc")
+    ap.add_argument("--seed0", type=int, default=0)
+    ap.add_argument("--build-keys", action="store_true",
+                    help="initialise from the networks the build's compute_kernel_distance_1d(PRNGKey(seed)) starts from")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     torch.set_num_threads(int(os.environ.get("CELL101_THREADS", max(1, min(8, os.cpu_count() or 1)))))
@@ -122,9 +129,12 @@ def main():
     rng = np.random.default_rng(7)
     for mode in a.modes.split(","):
         res = []
-        for seed in range(a.n_keys):
+        for seed in range(a.seed0, a.seed0 + a.n_keys):
             t1 = time.time()
-            model, it, gn = train(seed, x, mode)
+            init = None
+            if a.build_keys:
+                init = _init_seed(split(PRNGKey(seed))[0])
+            model, it, gn = train(seed, x, mode, init_seed=init)
             r = analyse(model, x, rng)
             res.append(r)
             say(f"2. [{mode:5s}] key {seed}: {it} steps, last clipped-grad norm {gn:.3g}; trained f: Lipschitz "
