@@ -133,6 +133,7 @@ __device__ __forceinline__ f32x4 ld4(const float* a) { return *(const f32x4*)a; 
 // MULTI = false: one step (sync_every = 1), the step loop compiled away.
 template <bool MULTI>
 __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParams p, int64_t n_chunks) {
+  const PooledStatsParams& p_outer = p;
   extern __shared__ __attribute__((aligned(16))) float lds[];
   constexpr int d = kF;
   constexpr int kSub = kFChunk / kFSub;  // sub-chunks per chunk
@@ -185,7 +186,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   uint4 rec = make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
   float pev = 0.0f;
   const bool ahead = p.xi != nullptr;
-  auto load_sub = [&](int64_t t) {
+  auto load_sub = [&](const PooledStatsParams& p, int64_t t) {
     const int64_t c0 = sub_c0(t);
     static_for<16>([&](auto N) {
       int64_t ch = c0 + w + 4 * N;
@@ -197,7 +198,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     kr = p.keys[2 * kc + ((lane >> 4) & 1)];
     if (ahead) rec = (kc < p.xi_cap) ? p.xrec[kc] : make_uint4(0xFFFFFFFFu, 0u, 0u, 0u);
   };
-  auto load_pe = [&](int64_t t) {
+  auto load_pe = [&](const PooledStatsParams& p, int64_t t) {
     const int64_t c0 = sub_c0(t);
     pev = (w == 0 && c0 + lane < p.C) ? p.pe[c0 + lane] : 0.0f;
   };
@@ -209,7 +210,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   // previous update launch when the chain's record is this draw's (i, key),
   // else here.  PRE: the rows are already in xr0 (sub-chunk 0: the prologue)
   float xr0[16];
-  auto noise_phase = [&](int64_t c0, auto PRE, int32_t its, uint32_t krv, bool records) {
+  auto noise_phase = [&](const PooledStatsParams& p, int64_t c0, auto PRE, int32_t its, uint32_t krv, bool records) {
     uint64_t usem = 0;
     if (ahead && records) {
       // lane N < 16: key word 0 of chain N is its own krv, word 1 lane N + 16's
@@ -271,8 +272,8 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   // its noise rows -- go out before the shared operands' (one memory latency
   // in the prologue instead of three)
   if (nmine > 0) {
-    load_sub(0);
-    load_pe(0);
+    load_sub(p, 0);
+    load_pe(p, 0);
     const int64_t c00 = sub_c0(0);
     if constexpr (kF64Pre0) static_for<16>([&](auto N) {
       int64_t ch = c00 + w + 4 * N;
@@ -305,8 +306,8 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
   }
   if (nmine > 0) {
     store_z();
-    if constexpr (kF64Pre0) noise_phase(sub_c0(0), std::true_type{}, it, kr, true);  // sub-chunk 0's phase (1), its rows already loaded
-    else noise_phase(sub_c0(0), std::false_type{}, it, kr, true);
+    if constexpr (kF64Pre0) noise_phase(p, sub_c0(0), std::true_type{}, it, kr, true);  // sub-chunk 0's phase (1), its rows already loaded
+    else noise_phase(p, sub_c0(0), std::false_type{}, it, kr, true);
   }
   lds_barrier();
   FS(14)
@@ -334,11 +335,12 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     asm volatile("" : "+v"(lane_o));
     const int lane = lane_o;
     const int h = lane >> 5, i = lane & 31;
+    const PooledStatsParams& p = reload_kernarg(p_outer);  // (SGPR pressure: reload_kernarg)
     Xi = (q & 1) ? XB : XA;
     Xp = (q & 1) ? XA : XB;
     // (records are for step 0: the update launch draws the next block's first step)
-    if ((t > 0 || s > 0) && !pre_ok) noise_phase(c0, std::false_type{}, it + s, kr, s == 0);
-    if (fin && more) load_sub(t + 1);  // in flight through phases (2) .. (6) of the last step
+    if ((t > 0 || s > 0) && !pre_ok) noise_phase(p, c0, std::false_type{}, it + s, kr, s == 0);
+    if (fin && more) load_sub(p, t + 1);  // in flight through phases (2) .. (6) of the last step
     FS(0)
     lds_barrier();
     FS(1)
@@ -406,7 +408,7 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
       }
       flag[lane] = acc_f;
       alph[lane] = a;
-      if (fin && more) load_pe(t + 1);
+      if (fin && more) load_pe(p, t + 1);
     }
     FS(6)
     lds_barrier();
@@ -429,21 +431,33 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
     // ---- (5) z' out, delta = z' - mu as [k][fperm chain] over the xi array
     //      (every LDS read first, then the stores)
     {
+      // LDS addresses from opaque per-lane bases + immediate offsets, and z'
+      // out through a buffer descriptor whose range ends at the sub-chunk's
+      // last valid chain: formed from the step's tile pointers directly, the
+      // 16 per-chain addresses went to SGPRs, spilled to VGPR lanes, and the
+      // phase ran ~200 v_readlane (r5l stamps: 6.9k of a sub-chunk's ~30k ticks)
+      uint32_t xp_a = lds_addr(Xp) + 4u * (uint32_t)(w * kFS + fperm(lane));
+      uint32_t zs_a = lds_addr(Zs) + 4u * (uint32_t)(w * kFS + lane);
+      uint32_t xi_a = lds_addr(Xi) + 4u * (uint32_t)(lane * kFS + 32 * (w & 1) + (w >> 1));
+      asm volatile("" : "+v"(xp_a), "+v"(zs_a), "+v"(xi_a));
+      typedef __attribute__((address_space(3))) float lds_f;
+      const lds_f* xpp = (const lds_f*)(uintptr_t)xp_a;
+      lds_f* zsp = (lds_f*)(uintptr_t)zs_a;
+      lds_f* xip = (lds_f*)(uintptr_t)xi_a;
       float zn[16];
       static_for<16>([&](auto N) {
         const int cc = w + 4 * N;
-        const float xp = Xp[cc * kFS + fperm(lane)], zo = Zs[cc * kFS + lane];
+        const float xp = xpp[4 * kFS * N], zo = zsp[4 * kFS * N];
         zn[N] = flag[cc] ? xp : zo;
       });
+      const int64_t rows = (int64_t)nv - w;  // chains w + 4 N < nv of this wave
+      const Buf zb(uniform_ptr(p.z_out + (c0 + w) * d), rows > 0 ? (uint32_t)rows * (uint32_t)d * 4u : 0u);
       static_for<16>([&](auto N) {
         const int cc = w + 4 * N;
-        float dv = 0.0f;
-        if (cc < nv) {
-          if (fin) p.z_out[(c0 + cc) * d + lane] = zn[N];
-          dv = zn[N] - mu_l;
-        }
-        if (!fin) Zs[cc * kFS + lane] = zn[N];  // the next step's z (this lane read the slot above)
-        Xi[lane * kFS + fperm(cc)] = dv;
+        if (fin) zb.st(zn[N], 4u * (uint32_t)lane, 4u * (uint32_t)(4 * d * N));  // (past nv: dropped)
+        const float dv = (cc < nv) ? zn[N] - mu_l : 0.0f;
+        if (!fin) zsp[4 * kFS * N] = zn[N];  // the next step's z (this lane read the slot above)
+        xip[2 * N] = dv;  // Xi[lane][fperm(w + 4 N)]: fperm(w + 4 N) = fperm(w) + 2 N
       });
     }
     FS(8)

@@ -812,6 +812,19 @@ __device__ __forceinline__ const void* uniform_ptr(const void* p) {
   return (const void*)(((uint64_t)hi << 32) | lo);
 }
 
+// The launch parameters re-read from the kernarg segment (scalar loads through
+// an opaque pointer) where a persistent loop would otherwise keep every field
+// live in SGPRs -- past the SGPR budget they spill to VGPR lanes, and each use
+// costs a v_readlane + hazard nop.  `p` must be the kernel's first argument.
+template <class T>
+__device__ __forceinline__ const T& reload_kernarg(const T& p) {
+  typedef __attribute__((address_space(4))) const T kconst_t;
+  kconst_t* pk = (kconst_t*)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  (void)p;
+  return *(const T*)pk;
+}
+
 // v_writelane through the LLVM intrinsic (no clang builtin in ROCm 7.2)
 __device__ int amh_writelane_i32(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 

@@ -1,22 +1,16 @@
 #!/bin/bash
-# Pooled-step A/B on one box: release library vs each variant library that
-# rebuilt amh_big_pooled.hip (lib/var_<name>/, tools/build_variants.sh), at
-# d = 64 (65,536 chains, configs[4] per GPU) and d = 256 (32,768 chains).
-# Usage (on the box): bash tools/gpu_ab_pooled.sh TAG VARIANT...
+# A/B of library variants on the pooled d = 64 step (K = 1): release vs
+# adaptive-mcmc_amd/lib/ab/libamh_<v>.so, alternated twice
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
-O=gpurun_out/${1:-abp}; shift
+O=gpurun_out/${1:-ab}; shift
 mkdir -p $O
 for rep in 1 2; do
-  for v in release "$@"; do
-    for cfg in "65536 64 400" "32768 256 100"; do
-      if [ $v = release ]; then
-        timeout -k 10 120 python3 tools/pooled_run.py $cfg > $O/p_${v}.txt 2>&1; r=$?
-      else
-        AMH_LIB_PATH=adaptive-mcmc_amd/lib/var_$v/libamh.so timeout -k 10 120 python3 tools/pooled_run.py $cfg > $O/p_${v}.txt 2>&1; r=$?
-      fi
-      echo "$v: $(grep pooled $O/p_${v}.txt)"
-      [ $r -eq 0 ] || exit $r
-    done
+  timeout -k 10 120 python3 tools/pooled_run.py 65536 64 400 1 > $O/rel_$rep.log 2>&1 || exit 10
+  echo "release: $(grep pooled $O/rel_$rep.log)"
+  for v in "$@"; do
+    AMH_LIB_PATH=adaptive-mcmc_amd/lib/ab/libamh_$v.so timeout -k 10 120 python3 tools/pooled_run.py 65536 64 400 1 > $O/${v}_$rep.log 2>&1 || exit 11
+    echo "$v: $(grep pooled $O/${v}_$rep.log)"
   done
 done
+exit 0
