@@ -935,6 +935,252 @@ __device__ __forceinline__ void s64_tie(T& a) { asm volatile("s_waitcnt lgkmcnt(
 template <class T>
 __device__ __forceinline__ void s64_tie(T& a, T& b) { asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a), "+v"(b)); }
 
+// lane J takes v (its own value), the others keep old -- capture<64, J> of a
+// broadcast of lane J's own value, without the v_readlane / v_writelane pair
+template <int J>
+__device__ __forceinline__ float s64_keep_at(float old, float v) {
+  float out;
+  unsigned long long m;
+  asm("s_lshl_b64 %1, 1, %4\n\tv_cndmask_b32_e64 %0, %2, %3, %1" : "=v"(out), "=&s"(m) : "v"(old), "v"(v), "n"(J));
+  return out;
+}
+
+// The d = 64 Gaussian potential (GaussianM<64>::potential, the same float
+// operations and order) with diff_j read back from the wave's scratch x_a
+// (one ds_write, then 16-B broadcast reads) instead of 64 v_readlane.
+__device__ __forceinline__ float s64_gauss_pot(float diff, uint32_t x_a, uint32_t prow, uint32_t r, float c0) {
+  s64_wr(x_a + r * 4u, diff);
+  f32x2v y01 = {0.0f, 0.0f}, y23 = {0.0f, 0.0f};
+  static_for<64 / kS64PB>([&](auto B) {
+    constexpr int b = B;
+    constexpr int NQ = kS64PB / 4;
+    f32x4 pv[NQ], dv[NQ];
+    static_for<NQ>([&](auto Q) {
+      pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
+      dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
+    });
+    if constexpr (NQ == 4) {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
+                   "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+    } else {
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+    }
+    static_for<2 * NQ>([&](auto K2) {
+      const f32x4 q = pv[(int)K2 / 2];
+      const f32x4 dq = dv[(int)K2 / 2];
+      const f32x2v pp = (K2 % 2 == 0) ? f32x2v{q[0], q[1]} : f32x2v{q[2], q[3]};
+      const f32x2v bp = (K2 % 2 == 0) ? f32x2v{dq[0], dq[1]} : f32x2v{dq[2], dq[3]};
+      if constexpr (K2 % 2 == 0) {
+        y01 = __builtin_elementwise_fma(pp, bp, y01);
+      } else {
+        y23 = __builtin_elementwise_fma(pp, bp, y23);
+      }
+    });
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  const float y = (y01[0] + y01[1]) + (y23[0] + y23[1]);
+  const float S = Grp<64>::sum(diff * y);
+  return (0.5f * S) + c0;
+}
+
+// asss_transition<64, GaussianM, true> (amh_asss.h; asss.py:197-251) for the
+// d = 64 persistent kernel: the same float operations in the same order (so
+// the same bits as the generic transition and orc_asss_step), with the
+// column broadcasts of the step64 ARWMH path -- the matrix-vector products
+// S z, S v and every potential read their broadcast vector from the wave's
+// LDS scratch, sweep 1 is s64_sweep1, sweep 2 the quarter-vector LDS scheme,
+// and the forward solve keeps one v_readlane per column (its own y_j by a
+// select).  The generic form spent ~576 + 64 (shrink steps + 2) v_readlane per
+// transition.
+__device__ __forceinline__ void asss_transition64(const StepParams& p, float (&U)[64], float& dl, float& x, float& mu,
+                                                  float& pe, float& asc, bool& updated, int32_t it, uint32_t k0,
+                                                  uint32_t k1, int r, const GaussianM<64>::Ctx& mctx, uint32_t x_a,
+                                                  uint32_t xq_a, uint32_t prow) {
+  using Gp = Grp<64>;
+  constexpr int d = 64;
+  const float sd = sqrtf((float)d);
+  const float epsd = p.eps * sd;
+  const float fd = (float)d;
+  const uint32_t ur = (uint32_t)r;
+  // ---- draws (asss.py:207, 219, 225, 60)
+  const amh_u32x4 o = amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_ASSS, k0, k1);
+  float v = amh_normal_from_bits(o.v[0]);
+  float vd = amh_normal_from_bits(Gp::template bcast_u<0>(o.v[1]));
+  const float ut = amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[2]));
+  const float th0 = 6.28318548f * amh_unif01_from_bits(Gp::template bcast_u<0>(o.v[3]));
+
+  // ---- y = S^-1 (x - mu)
+  const float e = dl * sd;
+  const float Dr = (dl + p.eps) * sd;
+  const float invD = 1.0f / Dr;
+  float b = x - mu;
+  float y = 0.0f;
+  static_for<d>([&](auto J) {
+    constexpr int j = J;
+    const float yl = b * invD;
+    y = s64_keep_at<j>(y, yl);
+    const float gj = Gp::template bcast<j>(yl * e);
+    b = fmaf(-U[j], gj, b);
+    column_fence<j>();
+  });
+
+  // ---- stereographic projection (asss.py:40-45)
+  const float ns = Gp::sum(y * y);
+  const float den = ns + 1.0f;
+  const float zr = (2.0f * y) / den;
+  const float zd = (ns - 1.0f) / den;
+
+  // ---- v orthogonal to z on S^d (asss.py:219-222), as amh_asss.h
+  const float dot = Gp::sum(v * zr) + (vd * zd);
+  v = fmaf(-dot, zr, v);
+  vd = fmaf(-dot, zd, vd);
+  const float nv = sqrtf(Gp::sum(v * v) + (vd * vd));
+  const bool degen = !(nv > 0.0f);
+  v = degen ? 0.0f : v / nv;
+  vd = degen ? 0.0f : vd / nv;
+
+  // ---- S z_1d and S v_1d: U times the broadcast vectors hz, hv from the scratch
+  auto svec = [&](float h) -> float {
+    s64_wr(x_a + ur * 4u, h);
+    float a4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    static_for<d / kS64EB>([&](auto B) {
+      constexpr int bb = B;
+      f32x4 ev[kS64EB / 4];
+      static_for<kS64EB / 4>([&](auto Q) { ev[(int)Q] = lds_ld4<16 * (kS64EB / 4 * bb + Q)>(x_a); });
+      if constexpr (kS64EB == 16) {
+        lds_wait(ev[0], ev[1], ev[2], ev[3]);
+      } else {
+        s64_tie(ev[0], ev[1]);
+      }
+      static_for<kS64EB>([&](auto K) {
+        constexpr int j = kS64EB * bb + K;
+        a4[j & 3] = fmaf(U[j], ev[(int)K / 4][(int)K % 4], a4[j & 3]);
+      });
+      __builtin_amdgcn_sched_barrier(0);
+    });
+    s64_wait();  // every lane's reads are done before the scratch is written again
+    return (a4[0] + a4[1]) + (a4[2] + a4[3]);
+  };
+  const float Sz = svec(e * zr) + epsd * zr;
+  const float Sv = svec(e * v) + epsd * v;
+
+  auto x_at = [&](float c, float s, float& om) -> float {
+    const float zdt = (zd * c) + (vd * s);
+    om = 1.0f - zdt;
+    return (((Sz * c) + (Sv * s)) / om) + mu;
+  };
+  auto pot = [&](float xv) -> float {
+    const float u = s64_gauss_pot(xv - mctx.mr, x_a, prow, ur, mctx.c0);
+    s64_wait();
+    return u;
+  };
+
+  // ---- slice level at z (asss.py:216-217, 224-226)
+  float om0;
+  const float x0 = x_at(1.0f, 0.0f, om0);
+  const float U0 = pot(x0);
+  const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
+
+  // ---- shrinkage (asss.py:59-96)
+  float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
+  int32_t iter = 0;
+  float xt, ux;
+  bool cont;
+  {
+    float s, c, om;
+    amh_sincosf(th, &s, &c);
+    xt = x_at(c, s, om);
+    ux = pot(xt);
+    float pt = ux + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    cont = !degen && ((pt > tpe) || (om < p.eps));
+  }
+  while (cont) {  // wave-uniform: one chain per wave
+    const float thmin_n = (th < 0.0f) ? th : thmin;
+    const float thmax_n = (th >= 0.0f) ? th : thmax;
+    const amh_u32x4 ok = amh_philox4x32_10((uint32_t)iter, (uint32_t)it, 1u, AMH_TAG_ASSS, k0, k1);
+    const float th_n = thmin_n + (thmax_n - thmin_n) * amh_unif01_from_bits(ok.v[0]);
+    float s, c, om;
+    amh_sincosf(th_n, &s, &c);
+    const float xn = x_at(c, s, om);
+    const float un = pot(xn);
+    float pt = un + fd * amh_logf(om);
+    if (amh_isnan(pt)) pt = INFINITY;
+    thmin = thmin_n;
+    thmax = thmax_n;
+    th = th_n;
+    xt = xn;
+    ux = un;
+    iter += 1;
+    cont = (iter < kAsssMaxIter) && ((pt > tpe) || (om < p.eps));
+  }
+  const bool capped = degen || iter >= kAsssMaxIter;  // asss.py:94: theta = 0
+  const float xnew = capped ? x0 : xt;
+  float pen = capped ? U0 : ux;
+  if (amh_isnan(pen)) pen = INFINITY;  // asss.py:234
+
+  // ---- adaptation (asss.py:237-251)
+  const int32_t itr = it + 1;
+  const int32_t n = (it < p.W) ? itr : itr - p.W;
+  const float gamma = lookup_gamma<64>(p, n);
+  const float delta = xnew - mu;
+  const float mun = mu + gamma * delta;
+  const float dmu = mun - mu;
+  const float locd = sqrtf(Gp::sum(dmu * dmu));
+
+  const float sq = sqrtf(1.0f - gamma);
+  const float ajj = sq * dl;
+  const float Dg = ajj * ajj;
+  const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
+  float ws = delta;  // sweep 1: lane r ends with w*_r (s64_sweep1)
+  static_for<d - 1>([&](auto J) {
+    s64_sweep1<J>(ws, U[J]);
+    column_fence<J>();
+  });
+  const float gw2 = gamma * (ws * ws);
+  const float tsc = gw2 / Dg;
+  const float bb = 1.0f + Gp::excl_scan(tsc, r);
+  const float g2 = (bb * Dg) + gw2;
+  const float dn = g2 / bb;
+  const float cc = (gamma * ws) / g2;
+  const float q = sqrtf(dn);
+  const float dnew = fmaf(cc, 0.0f, one) * q;
+  const bool revert = Gp::any(amh_isnan(dnew));
+  float sdiff = 0.0f;
+  if (!revert) {
+    const float ac = q - dl;
+    const float bc = cc * q;
+    float s4[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+    float w = delta;
+    static_for<16>([&](auto G4) {
+      constexpr int g = G4;
+      if constexpr (g % 4 == 0) s64_wr4_quarter<g / 4>(xq_a, ws, cc, ac, bc);
+      constexpr int gq = g % 4;
+      f32x4 cw = lds_ld4<16 * gq>(x_a), cv = lds_ld4<64 + 16 * gq>(x_a);
+      f32x4 ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
+      lds_wait(cw, cv, ca, cb);
+      static_for<4>([&](auto Q) {
+        constexpr int j = 4 * g + Q;
+        const float uo = U[j];
+        w = fmaf(-cw[(int)Q], uo, w);
+        const float un = fmaf(cv[(int)Q], w, uo);
+        const float tt = fmaf(uo, ca[(int)Q], cb[(int)Q] * w);
+        s4[j & 3] = fmaf(tt, tt, s4[j & 3]);
+        U[j] = un;
+      });
+      column_fence<g, 2>();
+    });
+    const float sacc = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    sdiff = sqrtf(Gp::sum(sacc));
+    dl = q;
+    updated = true;
+  }
+  asc = locd + sdiff;  // asss.py:248-250
+  x = xnew;
+  pe = pen;
+  mu = mun;
+}
+
 // kASSS: the same persistent data movement around one ASSS transition
 // (asss_transition, amh_asss.h; asss.py:197-251) instead of the ARWMH one --
 // the state is the same but for mean_accept_prob / log_step_size (absent).
@@ -1121,7 +1367,11 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
     bool updated = false;
     for (int32_t t = 0; t < p.n_steps; ++t) {
      if constexpr (kASSS) {
+#if AMH_S64_ASSS_GENERIC
       asss_transition<64, GaussianM, true>(p, U, dl, z, mu, pe, asc, updated, it, k0, k1, D, r, r, true, mctx, lds);
+#else
+      asss_transition64(p, U, dl, z, mu, pe, asc, updated, it, k0, k1, r, mctx, x_a, xq_a, prow);
+#endif
       it += 1;
      } else {
       // ---- noise (arwmh.py:162-165, 174): stream position = state.i
