@@ -1,0 +1,13 @@
+#!/bin/bash
+# Round-5 final evidence on the current build: the GPU suite, smoke(), and
+# bench.py --configs (every single-GPU config line)
+cd "$GRAFT_REPO_ROOT" || exit 1
+export TMPDIR=/tmp
+O=gpurun_out/${1:-r5final}
+mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1
+rc=$?; echo "tests rc=$rc"; tail -3 $O/pytest_gpu.log
+[ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $O/smoke.log 2>&1 || exit 10
+tail -2 $O/smoke.log
+exit 0
