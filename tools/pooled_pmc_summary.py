@@ -5,7 +5,7 @@ rows are read that way, MI355X_MICROARCH.md) and WRITE_SIZE (KiB) per launch
 of each pooled kernel, averaged over the last N launches, and the step's
 total against the algorithmic B_B(64) = 2 * 4 * (64 + 3) = 536 B per
 chain-step.
-  python3 tools/pooled_pmc_summary.py gpurun_out/<tag> [--chains 65536] [--last 20]"""
+  python3 tools/pooled_pmc_summary.py gpurun_out/<tag> [--chains 65536] [--last 20] [--k K]"""
 import argparse
 import collections
 import csv
@@ -31,8 +31,9 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--chains", type=int, default=65536)
     ap.add_argument("--last", type=int, default=20)
+    ap.add_argument("--k", type=int, default=1, help="sync_every of the run: one stats + one update launch per K steps")
     a = ap.parse_args()
-    out = {"chains": a.chains, "dim": 64, "B_B_bytes_per_step": a.chains * 536, "kernels": {}}
+    out = {"chains": a.chains, "dim": 64, "sync_every": a.k, "B_B_bytes_per_step": a.chains * 536, "kernels": {}}
     fetch, write = per_kernel(a.dir, "FETCH_SIZE"), per_kernel(a.dir, "WRITE_SIZE")
     total = 0.0
     for k in sorted(set(fetch) | set(write)):
@@ -44,8 +45,8 @@ def main():
         wb = 1024 * sum(w) / max(len(w), 1)
         out["kernels"][k] = {"read_bytes_corrected": fb, "write_bytes": wb, "launches": len(f)}
         total += fb + wb
-    out["traffic_bytes_per_step"] = total
-    out["traffic_over_B_B"] = total / out["B_B_bytes_per_step"]
+    out["traffic_bytes_per_step"] = total / a.k  # (per launch pair) / K
+    out["traffic_over_B_B"] = out["traffic_bytes_per_step"] / out["B_B_bytes_per_step"]
     print(json.dumps(out, indent=1))
 
 
