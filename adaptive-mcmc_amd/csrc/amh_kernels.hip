@@ -186,20 +186,6 @@ __device__ __forceinline__ void lds_st4(uint32_t a, f32x4 v) {
   asm volatile("ds_write_b128 %0, %1" : : "v"(a), "v"(v) : "memory");
 }
 
-#ifndef AMH_KARG_RELOAD
-#define AMH_KARG_RELOAD 1
-#endif
-typedef __attribute__((address_space(4))) const StepParams kconst_step_params;
-__device__ __forceinline__ const StepParams& reload_params(const StepParams& p) {
-#if AMH_KARG_RELOAD
-  kconst_step_params* pk = (kconst_step_params*)__builtin_amdgcn_kernarg_segment_ptr();
-  asm volatile("" : "+s"(pk));
-  return *(const StepParams*)pk;
-#else
-  return p;
-#endif
-}
-
 // DFIX > 0: d fixed at compile time below the group width (the diamonds
 // split path, d = 26 in groups of 32): column offsets become immediates.
 template <int DMAX, template <int> class M, bool EXACT, int DFIX = 0>
@@ -227,18 +213,12 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
   const float* wm = wz + wbuf_zd(CPW, d);
   const float* wsc = wm + wbuf_zd(CPW, d);
   const uint32_t oob = kOOB;
-#ifndef AMH_LDS_S2
-#define AMH_LDS_S2 1
-#endif
-#ifndef AMH_LDS_SP
-#define AMH_LDS_SP 1
-#endif
-#ifndef AMH_LDS_NB
-#define AMH_LDS_NB 4
-#endif
-  constexpr bool kLdsS2 = G == 32 && DFIX > 0 && AMH_LDS_S2;
-  constexpr bool kLdsSP = G == 32 && DFIX > 0 && (!kExt || AMH_LDS_SP > 1) && AMH_LDS_SP;
-  constexpr int NB = AMH_LDS_NB;
+  // G = 32 at a fixed d: sweep 2 and the next proposal's broadcasts through
+  // the wave's LDS scratch (the next-proposal form spilled in the ExtPotM
+  // instance, 128 VGPRs, so it keeps the one-swap DPP broadcasts there)
+  constexpr bool kLdsS2 = G == 32 && DFIX > 0;
+  constexpr bool kLdsSP = G == 32 && DFIX > 0 && !kExt;
+  constexpr int NB = 4;  // columns per LDS wait
   [[maybe_unused]] const uint32_t bs_a =
       lds_addr(lds + bcast_off<G, M>(p.model, d) + (size_t)wave_in_block * kBcastFloats);
 
@@ -373,7 +353,7 @@ __global__ __launch_bounds__(kBlockStep) void arwmh_step_kernel(StepParams p) {
     // (scalar loads through an opaque pointer): kept live across the loop,
     // their ~60 SGPRs spilled to VGPR lanes and every item paid hundreds of
     // v_readlane / v_writelane + hazard nops
-    const StepParams& p = reload_params(p_outer);
+    const StepParams& p = reload_kernarg(p_outer);
     const int r = lane & (G - 1);
     const int rr = r;
     const bool act = r < d;
