@@ -267,8 +267,15 @@ __global__ __launch_bounds__(256) void diamonds_pack_kernel(const float* __restr
   }
 }
 
-template <int KC>
-__global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) {
+// NB B tiles (32 chains each) per wave share every A tile.  NB = 4 halves
+// the A / Y operand loads per chain and doubles the wave's independent MFMA
+// chains, but at two waves per SIMD instead of three it was slower: 0.995
+// against 0.956 ms per transition (tools/gpu_ab_dia.sh, r5x).  (This form of
+// the NB = 2 kernel keeps its per-chain operands in registers where the
+// previous one moved 30 dwords through scratch in every tile: 0.976 -> 0.956.)
+constexpr int kDiaNB = 2;
+template <int KC, int NB>
+__global__ __launch_bounds__(256, (NB == 2 ? 2 : 1)) void diamonds_pot_mfma_kernel(PotParams p) {
   using T = DiaMfma<KC>;
   constexpr int S = T::S, G = T::G;
   const int d = p.d;
@@ -278,55 +285,54 @@ __global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) 
   const int lane = lane_id();
   const int i = lane & 31, h = lane >> 5;
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
-  const int64_t cb = ((int64_t)blockIdx.x * 4 + w) * 64;
-  const int64_t c0 = cb + i, c1 = cb + 32 + i;
-  const float* z0 = p.z + (c0 < n_ch ? c0 : n_ch - 1) * d;
-  const float* z1 = p.z + (c1 < n_ch ? c1 : n_ch - 1) * d;
-  float B0[S], B1[S];
-  static_for<S>([&](auto Q) {
-    const int k = 2 * Q + h;
-    B0[Q] = k < KC ? z0[1 + k] : 0.0f;
-    B1[Q] = k < KC ? z1[1 + k] : 0.0f;
+  const int64_t cb = ((int64_t)blockIdx.x * 4 + w) * (32 * NB);
+  int64_t cq[NB];
+  const float* zq[NB];
+  float B[NB][S];
+  float icq[NB], isq[NB];
+  static_for<NB>([&](auto J) {
+    cq[J] = cb + 32 * J + i;
+    zq[J] = p.z + (cq[J] < n_ch ? cq[J] : n_ch - 1) * d;
+    static_for<S>([&](auto Q) {
+      const int k = 2 * Q + h;
+      B[J][Q] = k < KC ? zq[J][1 + k] : 0.0f;
+    });
+    icq[J] = zq[J][0];
+    isq[J] = 1.0f / amh_expf(zq[J][KC + 1]);
   });
-  const float icpt0 = z0[0], icpt1 = z1[0];
-  const float isg0 = 1.0f / amh_expf(z0[KC + 1]), isg1 = 1.0f / amh_expf(z1[KC + 1]);
   const f32x4* xa = (const f32x4*)p.xpack + lane;
   const f32x4* ya = (const f32x4*)(p.xpack + NT * G * 256) + 4 * h;
-  float part0[16], part1[16];
-  static_for<16>([&](auto R) {
-    part0[R] = 0.0f;
-    part1[R] = 0.0f;
-  });
+  float part[NB][16];
+  static_for<NB>([&](auto J) { static_for<16>([&](auto R) { part[J][R] = 0.0f; }); });
   f32x4 a[G], y[4];
   static_for<G>([&](auto Q) { a[Q] = xa[64 * Q]; });
   static_for<4>([&](auto Q) { y[Q] = ya[Q]; });
-  // one tile: KC/2 MFMA pairs, then the residues; FULL: every row exists
-  // (all tiles but the last: no per-register row test)
+  // one tile: KC/2 MFMA steps for each B tile, then the residues; FULL: every
+  // row exists (all tiles but the last: no per-register row test)
   auto tile = [&](int64_t m, auto FULL) {
     f32x4 an[G], yn[4];
     const int64_t mn = (m + 1 < NT) ? m + 1 : m;  // next tile's loads in flight during this one
     static_for<G>([&](auto Q) { an[Q] = xa[(mn * G + Q) * 64]; });
     static_for<4>([&](auto Q) { yn[Q] = ya[8 * mn + Q]; });
-    f32x16 acc0 = f32x16{}, acc1 = f32x16{};
+    f32x16 acc[NB];
+    static_for<NB>([&](auto J) { acc[J] = f32x16{}; });
     static_for<S>([&](auto Q) {
       const float av = a[Q / 4][Q % 4];
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B0[Q], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B1[Q], acc1, 0, 0, 0);
+      static_for<NB>([&](auto J) { acc[J] = __builtin_amdgcn_mfma_f32_32x32x2f32(av, B[J][Q], acc[J], 0, 0, 0); });
     });
     const int64_t nrem = N - 32 * m;  // rows of this tile that exist
     static_for<16>([&](auto R) {
       const int rr = (R & 3) + 8 * (R >> 2) + 4 * h;
       const float yv = y[R / 4][R % 4];
-      const float e0 = (yv - (icpt0 + acc0[(int)R])) * isg0;
-      const float e1 = (yv - (icpt1 + acc1[(int)R])) * isg1;
-      if constexpr (decltype(FULL)::value) {
-        part0[R] = fmaf(e0, e0, part0[R]);
-        part1[R] = fmaf(e1, e1, part1[R]);
-      } else {
-        const bool ok = rr < nrem;
-        part0[R] = ok ? fmaf(e0, e0, part0[R]) : part0[R];
-        part1[R] = ok ? fmaf(e1, e1, part1[R]) : part1[R];
-      }
+      static_for<NB>([&](auto J) {
+        const float e = (yv - (icq[J] + acc[J][(int)R])) * isq[J];
+        if constexpr (decltype(FULL)::value) {
+          part[J][R] = fmaf(e, e, part[J][R]);
+        } else {
+          const bool ok = rr < nrem;
+          part[J][R] = ok ? fmaf(e, e, part[J][R]) : part[J][R];
+        }
+      });
     });
     static_for<G>([&](auto Q) { a[Q] = an[Q]; });
     static_for<4>([&](auto Q) { y[Q] = yn[Q]; });
@@ -339,44 +345,47 @@ __global__ __launch_bounds__(256, 2) void diamonds_pot_mfma_kernel(PotParams p) 
   for (int64_t m = 0; m + 1 < NT; ++m) tile(m, std::true_type{});
   if (NT > 0) tile(NT - 1, std::false_type{});
 #endif
-  // lane (i, 0) finishes chain c0, lane (i, 1) chain c1: the other half's
-  // residues arrive by a 32-lane swap
-  float all[32];
-  static_for<16>([&](auto R) {
-    const float mine = h ? part1[R] : part0[R];
-    const float other = __shfl_xor(h ? part0[R] : part1[R], 32, 64);
-    const int rm = (R & 3) + 8 * (R >> 2);
-    if (h == 0) {
-      all[rm] = mine;
-      all[rm + 4] = other;
-    } else {
-      all[rm + 4] = mine;
-      all[rm] = other;
-    }
+  // chain pair (2P, 2P + 1): lane (i, 0) finishes chain 2P, lane (i, 1) chain
+  // 2P + 1; the other half's residues arrive by a 32-lane swap
+  static_for<NB / 2>([&](auto PP) {
+    constexpr int P0 = 2 * PP, P1 = 2 * PP + 1;
+    float all[32];
+    static_for<16>([&](auto R) {
+      const float mine = h ? part[P1][R] : part[P0][R];
+      const float other = __shfl_xor(h ? part[P0][R] : part[P1][R], 32, 64);
+      const int rm = (R & 3) + 8 * (R >> 2);
+      if (h == 0) {
+        all[rm] = mine;
+        all[rm + 4] = other;
+      } else {
+        all[rm + 4] = mine;
+        all[rm] = other;
+      }
+    });
+    const float Ssum = butterfly32(all);
+    const int64_t c = h ? cq[P1] : cq[P0];
+    const float* zc = h ? zq[P1] : zq[P0];
+    float bb[32];
+    static_for<32>([&](auto R) {
+      constexpr int r = R;
+      if constexpr (r >= 1 && r <= KC) {
+        const float br = zc[r];
+        bb[r] = br * br;
+      } else {
+        bb[r] = 0.0f;
+      }
+    });
+    const float Bsum = butterfly32(bb);
+    const float icpt = zc[0];
+    const float ls = zc[KC + 1];
+    const float sg = amh_expf(ls);
+    const float cst = -3.30347394261755545f;
+    const float ll = fmaf(-0.5f, Ssum, (float)N * ((-ls) - HALF_LOG_2PI));
+    const float lpb = fmaf(-0.5f, Bsum, -(float)KC * HALF_LOG_2PI);
+    const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
+    const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
+    if (c < n_ch) p.pe[c] = -(((ll + lpb) + lpi) + lps);
   });
-  const float Ssum = butterfly32(all);
-  const int64_t c = h ? c1 : c0;
-  const float* zc = h ? z1 : z0;
-  float bb[32];
-  static_for<32>([&](auto R) {
-    constexpr int r = R;
-    if constexpr (r >= 1 && r <= KC) {
-      const float br = zc[r];
-      bb[r] = br * br;
-    } else {
-      bb[r] = 0.0f;
-    }
-  });
-  const float Bsum = butterfly32(bb);
-  const float icpt = zc[0];
-  const float ls = zc[KC + 1];
-  const float sg = amh_expf(ls);
-  const float cst = -3.30347394261755545f;
-  const float ll = fmaf(-0.5f, Ssum, (float)N * ((-ls) - HALF_LOG_2PI));
-  const float lpb = fmaf(-0.5f, Bsum, -(float)KC * HALF_LOG_2PI);
-  const float lpi = lp_student3(icpt, 8.0f, 10.0f, cst);
-  const float lps = (0.693147181f + lp_student3(sg, 0.0f, 10.0f, cst)) + ls;
-  if (c < n_ch) p.pe[c] = -(((ll + lpb) + lpi) + lps);
 }
 
 int64_t diamonds_pack_floats(int64_t N, int64_t K) {
@@ -408,7 +417,9 @@ hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
 hipError_t run_potential_lane(int model_id, const PotParams& p, hipStream_t s) {
   if (!split_model(model_id, p.d)) return hipErrorInvalidValue;
   if (p.xpack != nullptr && p.model.k - 1 == kDiaMfmaKc && p.d == kDiaMfmaKc + 2) {
-    hipLaunchKernelGGL(diamonds_pot_mfma_kernel<kDiaMfmaKc>, dim3((unsigned)((p.n + 255) / 256)), dim3(256), 0, s, p);
+    constexpr int per_block = 4 * 32 * kDiaNB;
+    hipLaunchKernelGGL((diamonds_pot_mfma_kernel<kDiaMfmaKc, kDiaNB>), dim3((unsigned)((p.n + per_block - 1) / per_block)),
+                       dim3(256), 0, s, p);
     return hipGetLastError();
   }
   const int64_t blocks = (p.n + 127) / 128;
