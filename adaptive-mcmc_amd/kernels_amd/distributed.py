@@ -88,6 +88,7 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
 # the update kernel follows the collective in stream order with no event.
 _NCCL_DTYPE = {torch.float64: 8, torch.float32: 7, torch.int32: 2, torch.int64: 4}
 _NCCL_SUM = 0
+_NCCL_IN_PROGRESS = 7  # ncclInProgress (non-blocking communicators)
 _rccl = None
 
 
@@ -113,6 +114,8 @@ def _rccl_lib():
         L.ncclAllReduce.restype = ctypes.c_int
         L.ncclGetErrorString.argtypes = [ctypes.c_int]
         L.ncclGetErrorString.restype = ctypes.c_char_p
+        L.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
+        L.ncclCommGetAsyncError.restype = ctypes.c_int
         _rccl = L
     return _rccl
 
@@ -142,5 +145,13 @@ def rccl_allreduce_sum(buf: torch.Tensor, comm: int, stream=None):
     s = stream if stream is not None else torch.cuda.current_stream(buf.device)
     L = _rccl_lib()
     rc = L.ncclAllReduce(buf.data_ptr(), buf.data_ptr(), buf.numel(), dt, _NCCL_SUM, comm, s.cuda_stream)
+    if rc == _NCCL_IN_PROGRESS:  # a non-blocking communicator: wait until the call is enqueued
+        import ctypes
+        st = ctypes.c_int(_NCCL_IN_PROGRESS)
+        while st.value == _NCCL_IN_PROGRESS:
+            rc = L.ncclCommGetAsyncError(comm, ctypes.byref(st))
+            if rc != 0:
+                break
+        rc = rc or st.value
     if rc != 0:
         raise RuntimeError(f"ncclAllReduce: {L.ncclGetErrorString(rc).decode()}")

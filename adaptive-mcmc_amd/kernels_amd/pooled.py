@@ -169,10 +169,18 @@ class PooledARWMH(ARWMH):
             return None
         if not self.overlap and not self.torch_stream_collective:
             from .distributed import rccl_allreduce_sum, rccl_comm_ptr
-            if self._rccl_comm is None:
-                self._rccl_comm = rccl_comm_ptr(self._group, buf.device)
-            rccl_allreduce_sum(buf, self._rccl_comm, torch.cuda.current_stream(dev))
-            return None
+            try:
+                if self._rccl_comm is None:
+                    self._rccl_comm = rccl_comm_ptr(self._group, buf.device)
+                rccl_allreduce_sum(buf, self._rccl_comm, torch.cuda.current_stream(dev))
+                return None
+            except (RuntimeError, OSError, AttributeError) as e:
+                # the same collective through torch's own stream from now on
+                # (slower by two cross-stream hops, same result)
+                import warnings
+                warnings.warn(f"RCCL on the compute stream unavailable ({e}); using torch.distributed's stream",
+                              RuntimeWarning)
+                self.torch_stream_collective = True
         if self._comm is None:
             self._comm = torch.cuda.Stream(device=dev)
         self._comm.wait_stream(torch.cuda.current_stream(dev))
