@@ -136,3 +136,22 @@ def test_mc_sd_formula():
     sd = M.mc_sd(vP, vQ, x, 100)
     want = np.sqrt(((vP + vQ) / 100)[1:] + ((vP + vQ) / 100)[:-1]) / np.diff(x)
     assert np.allclose(sd, want)
+
+
+def test_cell101_training_restatement_runs():
+    """tools/cell101_exact.py: a few steps of the float64 restatement of the
+    reference's training (lipschitz.py:396-491) on the exact objective and on
+    Monte Carlo draws; the trained f stays 1-Lipschitz and its exact ratios
+    stay below the pairs' Kantorovich-Rubinstein suprema."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import cell101_exact as T
+    x = np.linspace(-5, 5, 100, dtype=np.float32).astype(np.float64)
+    kr = M.kr_bound(x, SP, SQ)
+    for mode in ("exact", "mc"):
+        model, it, gn = T.train(0, x, mode, steps=3, n_samp=200)
+        assert it == 3 and np.isfinite(gn)
+        r = T.analyse(model, x, np.random.default_rng(0), n_mc=200)
+        assert r["lip"] <= 1.0 + 1e-6
+        assert 0.0 < r["rho_exact"] <= kr.max()
