@@ -391,7 +391,7 @@ def cpu_baseline(g, d: int, budget_s: float = 12.0):
 # GPU and CPU chain-steps/s, the speed-up, ESS/s and the roofline).  Synthetic
 # data of the reference shapes.
 CONFIG_NAMES = ("diamonds", "diamonds_ss", "gauss256", "gauss256_pooled", "gauss256_pooled_k16", "pooled64",
-                "pooled64_k16", "asss64", "asss_es", "pnx")
+                "pooled64_k16", "asss64", "asss256", "asss_es", "pnx")
 DIAMONDS_FLOPS = 2 * 5000 * 24 + 20000  # contraction + residual terms per chain-step
 
 
@@ -625,6 +625,13 @@ def configs_main(names, steps):
         k = ASSS(potential_fn=g, num_chains=65536, device=dev)
         emit(config_regime_a("ASSS d=64 correlated Gaussian", k, 65536, 64, {}, steps, dev, _orc_model("gaussian", g),
                              "hbm", asss=True))
+    if "asss256" in want:
+        # not a BASELINE config: ASSS past d = 64 (the large-d kernel, DESIGN.md
+        # §3.6) on configs[3]'s target and chain count
+        g = P.correlated_gaussian(256, log10_kappa=4.0)
+        k = ASSS(potential_fn=g, num_chains=32768, device=dev)
+        emit(config_regime_a("ASSS d=256 correlated Gaussian, kappa=1e4 (large-d kernel)", k, 32768, 256, {}, steps,
+                             dev, _orc_model("gaussian", g), "hbm", asss=True))
     if "asss_es" in want:
         data = dict(P.EIGHT_SCHOOLS_DATA)
         k = ASSS(model=P.eight_schools, num_chains=262144, device=dev)
