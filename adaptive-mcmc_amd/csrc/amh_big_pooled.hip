@@ -224,8 +224,11 @@ __global__ __launch_bounds__(256, 2) void pooled_fused64_kernel(PooledStatsParam
       // past C read 0 -- unused): 64-bit per-lane addresses here were hoisted
       // out of the step loop and spilled, 16 of them
       const int64_t cw = c0 + w;
+      // range: the rows this wave reads (cw + 4 N, N < 16: at most 64) -- the
+      // byte count stays below 2^32 for any C
       const int64_t nrow = p.C - cw;
-      const Buf xb(uniform_ptr(p.xi + cw * d), (uint32_t)((nrow > 0 ? nrow : 0) * d) * 4u);
+      const int64_t nr = nrow < 64 ? (nrow > 0 ? nrow : 0) : 64;
+      const Buf xb(uniform_ptr(p.xi + cw * d), (uint32_t)(nr * d) * 4u);
       static_for<16>([&](auto N) {
         if constexpr (decltype(PRE)::value) {
           xr[N] = xr0[N];

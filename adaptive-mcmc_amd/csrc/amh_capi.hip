@@ -182,7 +182,10 @@ int amh_destroy(amh_handle* h) {
   int rc = AMH_OK;
   if (h) {
     (void)hipSetDevice(h->device);
-    (void)hipDeviceSynchronize();  // the handle's last launches may still write its flag
+    // no device-wide synchronisation here (destroy runs from
+    // finalisers): the flag is read as it stands; a launch still in flight is
+    // covered by amh_check_device after the caller synchronised its stream.
+    // hipFree below orders the frees after outstanding work as HIP defines.
     if (h->err_host && *(volatile int*)h->err_host != 0) rc = fail(nullptr, AMH_EHIP, kUpdateStuck);
     if (h->gamma_tab) (void)hipFree(h->gamma_tab);
     if (h->partials) (void)hipFree(h->partials);

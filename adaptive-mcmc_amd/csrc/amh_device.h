@@ -199,9 +199,14 @@ __device__ __forceinline__ void step_noise(int r, int d, uint32_t it, uint32_t k
 // One chain per wave at d = 64 (arwmh_step64_kernel): lane r computes call
 // r >> 2 itself (four lanes the same call -- no cross-lane traffic, and the
 // registers of the bpermute form, which made the kernel spill) and keeps word
-// r & 3; u's call 16 runs on the scalar unit (the key and position are
-// wave-uniform).  The same bits as step_noise<64>.
+// r & 3.  u is word 64 (call 16): lane 63 computes call 16 instead of a
+// fourth copy of call 15 and takes its own word (word 3 of call 15) from lane
+// 60 -- two v_readlane and two selects instead of a second Philox call (the
+// round-5 form ran call 16 on the scalar unit: ~60 more instructions per
+// chain-step, AMH_S64_NOISE_SCALAR=1 keeps it for A/B).  The same bits as
+// step_noise<64>.
 __device__ __forceinline__ void step_noise_w64(int r, uint32_t it, uint32_t k0, uint32_t k1, float& xi, float& u) {
+#if AMH_S64_NOISE_SCALAR
   const amh_u32x4 o = amh_philox4x32_10((uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
   const int q = r & 3;
   const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
@@ -210,6 +215,16 @@ __device__ __forceinline__ void step_noise_w64(int r, uint32_t it, uint32_t k0, 
   const uint32_t ks1 = (uint32_t)__builtin_amdgcn_readfirstlane((int)k1);
   const uint32_t its = (uint32_t)__builtin_amdgcn_readfirstlane((int)it);
   u = amh_unif01_from_bits(amh_philox4x32_10(16u, its, 0u, AMH_TAG_STEP, ks0, ks1).v[0]);
+#else
+  const bool l63 = (r == 63);
+  const amh_u32x4 o = amh_philox4x32_10(l63 ? 16u : (uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
+  const int q = r & 3;
+  const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
+  const uint32_t w63 = (uint32_t)__builtin_amdgcn_readlane((int)o.v[3], 60);  // word 63
+  const uint32_t ub = (uint32_t)__builtin_amdgcn_readlane((int)o.v[0], 63);   // word 64
+  xi = amh_normal_from_bits(l63 ? w63 : w);
+  u = amh_unif01_from_bits(ub);
+#endif
 }
 
 // The same stream for one chain per wave with lane l owning rows 64 K + l

@@ -82,14 +82,22 @@ def max_over_ranks(x: float, device=None, group=None) -> float:
 # of its own, fenced to the caller's stream by events in both directions.  On
 # the pooled step's critical path (stats -> all_reduce -> update)
 # those two cross-queue hops cost ~29 us on MI355X (profiles/r5a_rccl_trace.txt)
-# against a 17 KB message.  rccl_allreduce_sum enqueues ncclAllReduce on the
-# caller's stream instead, with the communicator torch created for the group
-# (ProcessGroupNCCL._comm_ptr) and the RCCL library torch itself loaded, so
-# the update kernel follows the collective in stream order with no event.
+# against a 17 KB message.  RcclComm is a communicator of this package's own
+# -- ncclGetUniqueId on the group's first rank, the 128-byte id broadcast over
+# torch.distributed, ncclCommInitRank on every rank -- in the RCCL library
+# torch already mapped (one RCCL instance per process), and its all_reduce is
+# enqueued on the caller's stream, so the update kernel follows the collective
+# in stream order with no event.  It never shares a communicator with torch's
+# own collectives (barrier, max_over_ranks, gather_chains), which keep torch's.
 _NCCL_DTYPE = {torch.float64: 8, torch.float32: 7, torch.int32: 2, torch.int64: 4}
 _NCCL_SUM = 0
-_NCCL_IN_PROGRESS = 7  # ncclInProgress (non-blocking communicators)
+_NCCL_ID_BYTES = 128
 _rccl = None
+
+
+class RcclError(RuntimeError):
+    """An RCCL call returned an error (after a collective may have been issued:
+    never retried or routed elsewhere, since the ranks would disagree)."""
 
 
 def _rccl_lib():
@@ -97,7 +105,7 @@ def _rccl_lib():
     if _rccl is None:
         import ctypes
         path = None
-        try:  # the librccl torch mapped (same library instance as the communicator)
+        try:  # the librccl torch mapped (the same library instance torch uses)
             with open("/proc/self/maps") as f:
                 for line in f:
                     p = line.split()[-1] if line.split() else ""
@@ -107,51 +115,110 @@ def _rccl_lib():
         except OSError:
             pass
         if path is None:
-            raise RuntimeError("librccl is not loaded by torch (no nccl process group?)")
+            raise OSError("librccl is not mapped into this process (torch without RCCL?)")
         L = ctypes.CDLL(path)
+        L.ncclGetUniqueId.argtypes = [ctypes.c_void_p]
+        L.ncclGetUniqueId.restype = ctypes.c_int
+        L.ncclCommInitRank.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, _UniqueId, ctypes.c_int]
+        L.ncclCommInitRank.restype = ctypes.c_int
+        L.ncclCommDestroy.argtypes = [ctypes.c_void_p]
+        L.ncclCommDestroy.restype = ctypes.c_int
         L.ncclAllReduce.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
                                     ctypes.c_void_p, ctypes.c_void_p]
         L.ncclAllReduce.restype = ctypes.c_int
         L.ncclGetErrorString.argtypes = [ctypes.c_int]
         L.ncclGetErrorString.restype = ctypes.c_char_p
-        L.ncclCommGetAsyncError.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_int)]
-        L.ncclCommGetAsyncError.restype = ctypes.c_int
         _rccl = L
     return _rccl
 
 
-def rccl_comm_ptr(group, device: torch.device) -> int:
-    """The ncclComm_t torch holds for `group` on `device` (initialised on
-    first use by one collective through torch)."""
-    pg = group if group is not None else dist.group.WORLD
-    be = pg._get_backend(device)
-    ptr = be._comm_ptr()
-    if not ptr:
-        t = torch.zeros(1, device=device)
-        dist.all_reduce(t, group=group)  # creates the communicator
-        torch.cuda.synchronize(device)
-        ptr = be._comm_ptr()
-    if not ptr:
-        raise RuntimeError("no RCCL communicator for this group")
-    return int(ptr)
+def _uid_type():
+    import ctypes
+
+    class UniqueId(ctypes.Structure):  # ncclUniqueId: 128 opaque bytes, passed by value
+        _fields_ = [("internal", ctypes.c_char * _NCCL_ID_BYTES)]
+    return UniqueId
+
+
+_UniqueId = _uid_type()
+
+
+def _check(L, rc: int, what: str):
+    if rc != 0:
+        raise RcclError(f"{what}: {L.ncclGetErrorString(rc).decode()} (ncclResult {rc})")
+
+
+def rccl_unique_id(group=None, device=None) -> bytes:
+    """ncclGetUniqueId on the group's first rank, broadcast to every rank of
+    the group over torch.distributed (gloo or nccl); returns the 128 bytes."""
+    import ctypes
+    rank = dist.get_rank(group)
+    raw = bytes(_NCCL_ID_BYTES)
+    if rank == 0:
+        L = _rccl_lib()
+        uid = _UniqueId()
+        _check(L, L.ncclGetUniqueId(ctypes.byref(uid)), "ncclGetUniqueId")
+        raw = ctypes.string_at(ctypes.addressof(uid), _NCCL_ID_BYTES)
+    on_dev = dist.get_backend(group) == "nccl"
+    t = torch.tensor(list(raw), dtype=torch.uint8, device=device if on_dev else "cpu")
+    src = dist.get_global_rank(group, 0) if group is not None else 0
+    dist.broadcast(t, src=src, group=group)
+    return bytes(t.cpu().tolist())
+
+
+class RcclComm:
+    """A blocking RCCL communicator over the ranks of `group` (one GPU each),
+    owned by this package (created here, destroyed by close()).
+
+    all_reduce_sum enqueues ncclAllReduce on a given stream and raises
+    RcclError on any non-success result -- there is no fallback once a
+    collective may have been issued, because a rank that retried elsewhere
+    would leave the others with a different collective count."""
+
+    def __init__(self, group=None, device=None):
+        import ctypes
+        if not dist.is_initialized():
+            raise RuntimeError("RcclComm needs an initialised torch.distributed group")
+        dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        self.device = dev
+        self.rank = dist.get_rank(group)
+        self.world = dist.get_world_size(group)
+        L = _rccl_lib()
+        uid = _UniqueId()
+        ctypes.memmove(ctypes.addressof(uid), rccl_unique_id(group, dev), _NCCL_ID_BYTES)
+        comm = ctypes.c_void_p()
+        with torch.cuda.device(dev.index):
+            _check(L, L.ncclCommInitRank(ctypes.byref(comm), self.world, uid, self.rank), "ncclCommInitRank")
+        self._ptr = comm.value
+
+    @property
+    def ptr(self) -> int:
+        if self._ptr is None:
+            raise RuntimeError("RcclComm is closed")
+        return self._ptr
+
+    def all_reduce_sum(self, buf: torch.Tensor, stream=None):
+        """In-place all_reduce(sum) of a contiguous device tensor on `stream`
+        (default: the current stream of buf's device)."""
+        rccl_allreduce_sum(buf, self.ptr, stream)
+
+    def close(self):
+        """ncclCommDestroy (waits for this communicator's outstanding work)."""
+        if self._ptr is not None:
+            L = _rccl_lib()
+            p, self._ptr = self._ptr, None
+            with torch.cuda.device(self.device.index):
+                _check(L, L.ncclCommDestroy(p), "ncclCommDestroy")
 
 
 def rccl_allreduce_sum(buf: torch.Tensor, comm: int, stream=None):
     """In-place all_reduce(sum) of a contiguous device tensor, enqueued on
-    `stream` (default: the current stream of buf's device) with RCCL."""
+    `stream` (default: the current stream of buf's device) with RCCL on the
+    blocking communicator `comm` (RcclComm.ptr).  Raises RcclError."""
     dt = _NCCL_DTYPE.get(buf.dtype)
     if dt is None or not buf.is_cuda or not buf.is_contiguous():
         raise ValueError("rccl_allreduce_sum: contiguous float64/float32/int device tensor expected")
     s = stream if stream is not None else torch.cuda.current_stream(buf.device)
     L = _rccl_lib()
-    rc = L.ncclAllReduce(buf.data_ptr(), buf.data_ptr(), buf.numel(), dt, _NCCL_SUM, comm, s.cuda_stream)
-    if rc == _NCCL_IN_PROGRESS:  # a non-blocking communicator: wait until the call is enqueued
-        import ctypes
-        st = ctypes.c_int(_NCCL_IN_PROGRESS)
-        while st.value == _NCCL_IN_PROGRESS:
-            rc = L.ncclCommGetAsyncError(comm, ctypes.byref(st))
-            if rc != 0:
-                break
-        rc = rc or st.value
-    if rc != 0:
-        raise RuntimeError(f"ncclAllReduce: {L.ncclGetErrorString(rc).decode()}")
+    _check(L, L.ncclAllReduce(buf.data_ptr(), buf.data_ptr(), buf.numel(), dt, _NCCL_SUM, comm, s.cuda_stream),
+           "ncclAllReduce")

@@ -168,19 +168,23 @@ class PooledARWMH(ARWMH):
             dist.all_reduce(buf, op=dist.ReduceOp.SUM, group=self._group)
             return None
         if not self.overlap and not self.torch_stream_collective:
-            from .distributed import rccl_allreduce_sum, rccl_comm_ptr
-            try:
-                if self._rccl_comm is None:
-                    self._rccl_comm = rccl_comm_ptr(self._group, buf.device)
-                rccl_allreduce_sum(buf, self._rccl_comm, torch.cuda.current_stream(dev))
+            # this package's own communicator (distributed.RcclComm), the
+            # collective on the compute stream.  Setup (the id broadcast and
+            # ncclCommInitRank) runs on every rank in the same host order;
+            # any RCCL error raises -- no fallback once a collective may have
+            # been issued.  Only a process without RCCL mapped (OSError, the
+            # same on every rank) takes torch's stream instead.
+            from .distributed import RcclComm
+            if self._rccl_comm is None:
+                try:
+                    self._rccl_comm = RcclComm(self._group, buf.device)
+                except OSError as e:
+                    import warnings
+                    warnings.warn(f"RCCL not mapped ({e}); using torch.distributed's stream", RuntimeWarning)
+                    self.torch_stream_collective = True
+            if self._rccl_comm is not None:
+                self._rccl_comm.all_reduce_sum(buf, torch.cuda.current_stream(dev))
                 return None
-            except (RuntimeError, OSError, AttributeError) as e:
-                # the same collective through torch's own stream from now on
-                # (slower by two cross-stream hops, same result)
-                import warnings
-                warnings.warn(f"RCCL on the compute stream unavailable ({e}); using torch.distributed's stream",
-                              RuntimeWarning)
-                self.torch_stream_collective = True
         if self._comm is None:
             self._comm = torch.cuda.Stream(device=dev)
         self._comm.wait_stream(torch.cuda.current_stream(dev))
@@ -189,6 +193,14 @@ class PooledARWMH(ARWMH):
             ev = torch.cuda.Event()
             ev.record(self._comm)
         return ev
+
+    def close_comm(self):
+        """Destroy this sampler's own RCCL communicator (collective over the
+        group's ranks in the same host order; a later multi-rank step creates
+        a new one)."""
+        if self._rccl_comm is not None:
+            c, self._rccl_comm = self._rccl_comm, None
+            c.close()
 
     def _stats(self, L, cin, sout, buf, C):
         dev = sout.z.device.index

@@ -28,7 +28,8 @@
  *     triangle packed column by column: column j holds rows j..d-1),
  *     scalars [C], rng_key [C][2] uint32.
  *   - All work is enqueued on `stream` (a hipStream_t; NULL = default
- *     stream).  No call synchronises the device except amh_destroy.
+ *     stream).  No call synchronises the device (amh_destroy's hipFree
+ *     calls wait for outstanding device work as HIP defines).
  *   - Return value: 0 on success, a negative AMH_E* code on failure;
  *     amh_last_error(h) describes the failure (thread-local when h is NULL).
  *   - One handle per device; handles are not shared between host threads.
@@ -113,8 +114,9 @@ int amh_destroy(amh_handle* h);
  * factor, so the run no longer follows the bit spec).  Returns AMH_EHIP with
  * the message in amh_last_error and clears the flag, else AMH_OK.  Reads a
  * host-mapped word, no synchronisation: a launch still in flight is covered
- * by a call after the caller has synchronised its stream (amh_destroy does
- * that itself and returns the same code).  No counterpart in the reference,
+ * by a call after the caller has synchronised its stream (amh_destroy reads
+ * the flag as it stands, without synchronising, and returns the same code
+ * when it is set).  No counterpart in the reference,
  * whose guards (arwmh.py:171, :191) cannot fail this way. */
 int amh_check_device(amh_handle* h);
 
