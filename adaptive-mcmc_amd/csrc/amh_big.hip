@@ -35,6 +35,9 @@ namespace {
 
 constexpr int kNS = 4;  // row slots per lane: d <= 64 * kNS
 constexpr int kAsssBigMaxIter = 50;  // asss.py:59 max_iterations
+#ifndef AMH_ABL_NOPASSD
+#define AMH_ABL_NOPASSD 0
+#endif
 
 __device__ __forceinline__ float rdl(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -96,11 +99,12 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         float* cur = (b & 1) ? wb1 : wb0;
         if (b + 1 < nb) issue_block(Lc, d, P, b + 1, (b & 1) ? wb0 : wb1, lane);
         const int64_t ob = col_off(d, kColBlk * b);
-        for (int q = 0; q < kColBlk; ++q) {
+        // element (r, j) sits at cur[col_off(d, j) - ob + r - j]; column q + 1's
+        // reads are issued before f runs on column q (one LDS round trip off
+        // each column but the block's first)
+        auto rd = [&](int q, float (&v)[kNS]) {
           const int j = kColBlk * b + q;
-          // element (r, j) sits at cur[col_off(d, j) - ob + r - j]
           const uint32_t a0 = lds_addr(cur) + 4u * (uint32_t)(col_off(d, j) - ob - j + lane);
-          float v[kNS];
           static_for<kNS>([&](auto K) {
             if constexpr (K >= kb) {
               v[K] = lds_ld1<0>(a0 + 256u * K);
@@ -108,8 +112,23 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
               v[K] = 0.0f;
             }
           });
-          lds_wait(v[0], v[1], v[2], v[3]);
-          f(KB, j, v);
+        };
+        // (the wait sits at the end of the iteration, so no loop-carried
+        // register is copied while its read is in flight)
+        float vn[kNS];
+        rd(0, vn);
+        lds_wait(vn[0], vn[1], vn[2], vn[3]);
+        for (int q = 0; q < kColBlk; ++q) {
+          float v[kNS];
+          static_for<kNS>([&](auto K) { v[K] = vn[K]; });
+#if AMH_BIG_NOPIPE
+          f(KB, kColBlk * b + q, v);
+          if (q + 1 < kColBlk) rd(q + 1, vn);
+#else
+          if (q + 1 < kColBlk) rd(q + 1, vn);
+          f(KB, kColBlk * b + q, v);
+#endif
+          lds_wait(vn[0], vn[1], vn[2], vn[3]);
         }
       }
     }
@@ -543,19 +562,22 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
 // ------------------------------------------------------------------ ASSS ----
 // ASSS (asss.py:192-269) for 64 < d <= 256, d % 32 == 0, dense Gaussian:
 // one wave per chain, lane l owns rows 64 s + l, the factor streamed column
-// by column through the wave's LDS double buffer (for_columns).  Four passes
-// over the factor per transition (bit spec: oracle asss_step_big1):
-//   A  y = S^-1 (x - mu), S = (L + eps I) sqrt(d): at column j lane j's
-//      y_j = b_j / D_j and g = y_j e_j go to every lane, rows r > j take
-//      b_r = fmaf(-U_rj, g, b_r)                            (asss.py:33-45)
-//   B  a = S z, b = S v: one accumulator per row in column order, the
-//      diagonal (U_rr = 1) at column r, then + eps sqrt(d) (z_r, v_r)
+// by column through the wave's LDS double buffer (for_columns).  Two passes
+// over the factor per transition (bit spec: oracle asss_step_big1; round 5
+// had four):
+//   A  one column sweep, at column j lane j's y_j = b_j / D_j (y = S^-1 (x -
+//      mu), S = (L + eps I) sqrt(d); asss.py:33-45) and three more running
+//      sums: av = U (e v) (S v = av + eps sqrt(d) v for the raw draw v),
+//      wy = U^-1 y and wv = U^-1 v (ADAPT only).  S y = x - mu, so S z =
+//      2 (x - mu) / den and S v_tangent = (S v - dot S z) / |v| need no pass
 //   -- the potential along the slice circle: Pa, Pb, Pg = P a, P b, P g
 //      (g = mu - m; P's rows read coalesced, an fmaf chain over k), then
 //      every shrink step is O(d): D = (a c + b s) / om + g, Y = (Pa c + Pb s)
 //      / om + Pg, U = 0.5 sum D Y + c0                      (asss.py:59-96)
-//   C  w = U^-1 delta            D  the rank-one update streaming L' out,
-//      as the large-d ARWMH step pass (no step size)   (asss.py:246-267)
+//   -- w = U^-1 delta without a pass: delta = S q, q = (z c + v s) / om at
+//      the accepted angle, so w = sqrt(d) (dl q + eps U^-1 q)
+//   D  the rank-one update streaming L' out, as the large-d ARWMH step pass
+//      (no step size)                                     (asss.py:246-267)
 // ADAPT = false is the frozen kernel of sample_Pnx (shared loc / factor).
 namespace {
 
@@ -582,29 +604,53 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   float vd = amh_normal_from_bits(o0.v[1]);
   const float ut = amh_unif01_from_bits(o0.v[2]);
   const float th0 = 6.28318548f * amh_unif01_from_bits(o0.v[3]);
-  // ---- pass A: y = S^-1 (x - mu)
-  float e[kNS], invD[kNS], b[kNS], y[kNS], tt[kNS];
+  // ---- pass A: y = S^-1 (x - mu), av = U (e v), wy = U^-1 y, wv = U^-1 v
+  float e[kNS], invD[kNS], b[kNS], y[kNS], tt[kNS], hv[kNS], av[kNS], ty[kNS], tv[kNS], wy[kNS], wv[kNS];
   static_for<kNS>([&](auto K) {
     const bool act = 64 * K + lane < d;
     e[K] = dl[K] * sd;
     invD[K] = 1.0f / ((dl[K] + eps) * sd);
     b[K] = act ? x[K] - mu[K] : 0.0f;
-    y[K] = 0.0f;
+    hv[K] = e[K] * v[K];
+    y[K] = av[K] = ty[K] = tv[K] = wy[K] = wv[K] = 0.0f;
   });
+#if !AMH_ABL_NOPASSA
   for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
     constexpr int kb = KB;
     const int jl = j - 64 * kb;
     const float yl = rdl(b[kb] * invD[kb], jl);
     const float g = yl * rdl(e[kb], jl);
+    const float hvj = rdl(hv[kb], jl);
     const float invj = rdl(inv[kb], jl);
-    if (lane == jl) y[kb] = yl;
+    float wyj = 0.0f, wvj = 0.0f;
+    if constexpr (ADAPT) {
+      wyj = yl - rdl(ty[kb], jl);
+      wvj = rdl(v[kb] - tv[kb], jl);
+    }
+    if (lane == jl) {
+      y[kb] = yl;
+      av[kb] = fmaf(1.0f, hvj, av[kb]);
+      wy[kb] = wyj;
+      wv[kb] = wvj;
+    }
     static_for<kNS>([&](auto K) {
       if constexpr (K >= kb) {
         const int r = 64 * K + lane;
-        if (r > j && r < d) b[K] = fmaf(-(vv[K] * invj), g, b[K]);
+        if (r > j && r < d) {
+          const float uo = vv[K] * invj;
+          b[K] = fmaf(-uo, g, b[K]);
+          av[K] = fmaf(uo, hvj, av[K]);
+          if constexpr (ADAPT) {
+            ty[K] = fmaf(uo, wyj, ty[K]);
+            tv[K] = fmaf(uo, wvj, tv[K]);
+          }
+        }
       }
     });
   });
+#endif
+  float svr[kNS];  // S v for the raw draw
+  static_for<kNS>([&](auto K) { svr[K] = av[K] + epsd * v[K]; });
   // ---- stereographic projection, tangent v (asss.py:40-45, 219-222)
   static_for<kNS>([&](auto K) { tt[K] = y[K] * y[K]; });
   const float ns = big_sum(tt);
@@ -621,42 +667,22 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   const bool degen = !(nv > 0.0f);  // the d <= 64 kernel's rule (amh_asss.h)
   static_for<kNS>([&](auto K) { v[K] = degen ? 0.0f : v[K] / nv; });
   vd = degen ? 0.0f : vd / nv;
-  // ---- pass B: a = S z, b = S v
-  float hz[kNS], hv[kNS], a[kNS], bb[kNS];
-  static_for<kNS>([&](auto K) {
-    hz[K] = e[K] * zr[K];
-    hv[K] = e[K] * v[K];
-    a[K] = bb[K] = 0.0f;
-  });
-  for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
-    constexpr int kb = KB;
-    const int jl = j - 64 * kb;
-    const float hzj = rdl(hz[kb], jl), hvj = rdl(hv[kb], jl), invj = rdl(inv[kb], jl);
-    if (lane == jl) {
-      a[kb] = fmaf(1.0f, hzj, a[kb]);
-      bb[kb] = fmaf(1.0f, hvj, bb[kb]);
-    }
-    static_for<kNS>([&](auto K) {
-      if constexpr (K >= kb) {
-        const int r = 64 * K + lane;
-        if (r > j && r < d) {
-          const float uo = vv[K] * invj;
-          a[K] = fmaf(uo, hzj, a[K]);
-          bb[K] = fmaf(uo, hvj, bb[K]);
-        }
-      }
-    });
-  });
-  float Sz[kNS], Sv[kNS], gm[kNS], Pa[kNS], Pb[kNS], Pg[kNS];
+  // ---- S z = 2 (x - mu) / den, S v = (S v_raw - dot S z) / |v|; U^-1 z, U^-1 v
+  float Sz[kNS], Sv[kNS], Wz[kNS], Wv[kNS], gm[kNS], Pa[kNS], Pb[kNS], Pg[kNS];
   static_for<kNS>([&](auto K) {
     const int r = 64 * K + lane;
     const bool act = r < d;
-    Sz[K] = a[K] + epsd * zr[K];
-    Sv[K] = bb[K] + epsd * v[K];
+    Sz[K] = act ? (2.0f * (x[K] - mu[K])) / den : 0.0f;
+    Sv[K] = (degen || !act) ? 0.0f : fmaf(-dot, Sz[K], svr[K]) / nv;
+    if constexpr (ADAPT) {
+      Wz[K] = (2.0f * wy[K]) / den;
+      Wv[K] = (degen || !act) ? 0.0f : fmaf(-dot, Wz[K], wv[K]) / nv;
+    }
     gm[K] = act ? mu[K] - m[act ? r : 0] : 0.0f;
     Pa[K] = Pb[K] = Pg[K] = 0.0f;
   });
   // ---- P a, P b, P g: row k of P (= column k) coalesced, k in order
+#if !AMH_ABL_NOPMV  // (timing ablations only: AMH_ABL_*)
   static_for<kNS>([&](auto KB) {
     constexpr int kb = KB;
     if (64 * kb < d) {
@@ -679,6 +705,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       }
     }
   });
+#endif
   // the point at angle (cs, sn) of the slice circle: x and U
   auto eval = [&](float cs, float sn, float (&xo)[kNS], float& om) -> float {
     om = 1.0f - ((zd * cs) + (vd * sn));
@@ -699,12 +726,15 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
   float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
   int32_t iter = 0;
-  float ux;
+  float ux, cst, snt, omt;  // the angle of xt
   bool cont;
   {
     float sn, cs, om;
     amh_sincosf(th, &sn, &cs);
     ux = eval(cs, sn, xt, om);
+    cst = cs;
+    snt = sn;
+    omt = om;
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
     cont = !degen && ((pt > tpe) || (om < eps));
@@ -717,12 +747,20 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     float sn, cs, om;
     amh_sincosf(th, &sn, &cs);
     ux = eval(cs, sn, xt, om);
+    cst = cs;
+    snt = sn;
+    omt = om;
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
     iter += 1;
     cont = (iter < kAsssBigMaxIter) && ((pt > tpe) || (om < eps));
   }
   const bool capped = degen || iter >= kAsssBigMaxIter;  // asss.py:94: theta = 0
+  if (capped) {
+    cst = 1.0f;
+    snt = 0.0f;
+    omt = om0;
+  }
   float xn[kNS];
   static_for<kNS>([&](auto K) { xn[K] = capped ? x0[K] : xt[K]; });
   float pen = capped ? U0 : ux;
@@ -738,7 +776,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   } else {
     // ---- adaptation (asss.py:246-267): mean, rank-one update, as_change
     const float gamma = gamma_in;
-    float delta[kNS], mun[kNS], Dg[kNS], one[kNS], ws[kNS], sw[kNS], gw2[kNS];
+    float delta[kNS], mun[kNS], Dg[kNS], one[kNS], ws[kNS], gw2[kNS];
     const float sq = sqrtf(1.0f - gamma);
     static_for<kNS>([&](auto K) {
       const bool act = 64 * K + lane < d;
@@ -749,23 +787,12 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       const float ajj = sq * dl[K];
       Dg[K] = ajj * ajj;
       one[K] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
-      sw[K] = ws[K] = 0.0f;
+      // w = U^-1 delta = sqrt(d) (dl q + eps U^-1 q), q = (z c + v s) / om
+      const float q = ((zr[K] * cst) + (v[K] * snt)) / omt;
+      const float wq = ((Wz[K] * cst) + (Wv[K] * snt)) / omt;
+      ws[K] = act ? ((dl[K] * q) + (eps * wq)) * sd : 0.0f;
     });
     const float locd = sqrtf(big_sum(tt));
-    // pass C: w = U^-1 delta
-    for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
-      constexpr int kb = KB;
-      const int jl = j - 64 * kb;
-      const float wj = rdl(delta[kb] - sw[kb], jl);
-      const float invj = rdl(inv[kb], jl);
-      if (lane == jl) ws[kb] = wj;
-      static_for<kNS>([&](auto K) {
-        if constexpr (K >= kb) {
-          const int r = 64 * K + lane;
-          if (r > j && r < d) sw[K] = fmaf(vv[K] * invj, wj, sw[K]);
-        }
-      });
-    });
     float cc[kNS], qq[kNS];
     bool bad = false;
     {
@@ -787,7 +814,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
         bad = bad || (act && amh_isnan(dnew));
       });
     }
-    const bool revert = __ballot(bad) != 0ull;
+    const bool revert = __ballot(bad) != 0ull || AMH_ABL_NOPASSD;
     float sdiff = 0.0f;
     if (!revert) {
       // pass D: the update, L' streamed out (in place allowed: block b + 1 is
@@ -825,7 +852,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
         });
       });
       sdiff = sqrtf(big_sum(sacc));
-    } else if (Lout != Lc) {  // factor kept (asss.py:255): copied verbatim
+    } else if (Lout != Lc && !AMH_ABL_NOPASSD) {  // factor kept (asss.py:255): copied verbatim
       for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
         constexpr int kb = KB;
         float* ocol = Lout + col_off(d, j) - j;

@@ -177,22 +177,30 @@ struct Grp {
 // lanes the same call: no cross-lane traffic, one call per lane as before)
 // and keeps word r & 3.  u is word d & 3 of call d >> 2, which lane
 // 4 (d >> 2) computed when that lane is in the group (d < G, or d % 4 != 0);
-// else (d = G, a multiple of 4) one more call.
+// else (d = G, a multiple of 4) lane G - 1 computes call d >> 2 instead of a
+// fourth copy of call G/4 - 1 and takes its own word from lane G - 4 (two
+// broadcasts instead of a second Philox call per lane).
 template <int G>
 __device__ __forceinline__ void step_noise(int r, int d, uint32_t it, uint32_t k0, uint32_t k1, float& xi, float& u) {
-  const amh_u32x4 o = amh_philox4x32_10((uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
-  const int q = r & 3;
-  const uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
-  xi = amh_normal_from_bits(w);
-  const int qd = d & 3;
   const int src = 4 * (d >> 2);
+  const bool full = src >= G;  // d == G: word d is in call G / 4, which no lane computes
+  const bool last = full && r == G - 1;
+  const amh_u32x4 o = amh_philox4x32_10(last ? (uint32_t)(d >> 2) : (uint32_t)(r >> 2), it, 0u, AMH_TAG_STEP, k0, k1);
+  const int q = r & 3;
+  uint32_t w = (q == 0) ? o.v[0] : ((q == 1) ? o.v[1] : ((q == 2) ? o.v[2] : o.v[3]));
   uint32_t ub;
-  if (src < G) {
+  if (!full) {
+    const int qd = d & 3;
     const uint32_t us = (qd == 0) ? o.v[0] : ((qd == 1) ? o.v[1] : ((qd == 2) ? o.v[2] : o.v[3]));
     ub = (uint32_t)__float_as_int(Grp<G>::bcast_rt(__int_as_float((int)us), src));
+  } else if constexpr (G >= 4) {  // (d <= G < 4 never fills a call)
+    const uint32_t wl = (uint32_t)__float_as_int(Grp<G>::bcast_rt(__int_as_float((int)o.v[3]), G - 4));
+    ub = (uint32_t)__float_as_int(Grp<G>::bcast_rt(__int_as_float((int)o.v[0]), G - 1));
+    w = last ? wl : w;
   } else {
-    ub = amh_philox4x32_10((uint32_t)(d >> 2), it, 0u, AMH_TAG_STEP, k0, k1).v[0];
+    ub = 0u;
   }
+  xi = amh_normal_from_bits(w);
   u = amh_unif01_from_bits(ub);
 }
 

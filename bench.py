@@ -536,7 +536,7 @@ def config_regime_a(name, kernel, C, d, kwargs, steps, dev, om, roof, ess_burn=0
         line["ess"]["burn_in"] = ess_burn
         line["ess"]["mean_accept_prob_after_burn_in"] = line["mean_accept_prob"] = (
             float(st.mean_accept_prob.mean()) if hasattr(st, "mean_accept_prob") else None)
-    if cpu:
+    if cpu and CONFIG_CPU:
         line["cpu_baseline"] = cpu_regime_a(om, C, asss=asss)
         line["speedup_vs_cpu"] = rate / line["cpu_baseline"]["value"]
     return line
@@ -583,10 +583,13 @@ def config_pooled(key, d, C, kappa, K, steps, dev, burn_in, ess=True, cpu=True):
                          "stats_kernel_frac": C * fl / (sms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS}}
     if ess and K == 1:
         line["ess"] = ess_window(k, st, 1000, [0, 1, d // 2, d - 1])
-    if cpu:
+    if cpu and CONFIG_CPU:
         line["cpu_baseline"] = cpu_pooled(_orc_model("gaussian", g), C, K)
         line["speedup_vs_cpu"] = rate / line["cpu_baseline"]["value"]
     return line
+
+
+CONFIG_CPU = True  # --configs --no-cpu-baseline: GPU lines only (A/B runs)
 
 
 def configs_main(names, steps):
@@ -695,6 +698,8 @@ def main():
     if args.configs is not None:
         if args.gpus != 1:
             raise SystemExit("--configs runs on one GPU")
+        global CONFIG_CPU
+        CONFIG_CPU = not args.no_cpu_baseline
         return configs_main(args.configs.split(","), args.steps if args.steps != 200 else 20)
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")

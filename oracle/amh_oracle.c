@@ -1564,18 +1564,29 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
 /* n_steps ASSS transitions of chains [0, C) in place (one kernel launch);
  * collect_z [n_steps][C][d] / collect_pe [n_steps][C] nullable. */
 /* ASSS for large dimensions (asss.py:192-269; 64 < d <= 256, d % 32 == 0,
- * the dense Gaussian; round 5).  Kernel mirror of amh_asss_big.hip: one wave
- * per chain, lane l owns rows 64 s + l, the factor streamed column by column
- * (the large-d ARWMH path's layout), four passes over it per transition:
- *   A  y = S^-1 (x - mu), S = (L + eps I) sqrt(d) (asss.py:214, :33-45):
- *      column j: y_j = b_j / D_j, g = y_j e_j, b_r = fmaf(-U_rj, g, b_r) (r > j)
- *   B  S z and S v in column order, one accumulator per row, the diagonal
- *      (U_rr = 1) at column r, then + eps sqrt(d) z_r (resp. v_r)
+ * the dense Gaussian; round 5, passes folded in round 6).  Kernel mirror of
+ * amh_big.hip asss_big_chain: one wave per chain, lane l owns rows 64 s + l,
+ * the factor streamed column by column (the large-d ARWMH path's layout),
+ * two passes over it per transition:
+ *   A  one column sweep, four accumulators per row (U = L / diag(L), unit
+ *      diagonal; S = (L + eps I) sqrt(d) = U diag(e) + eps sqrt(d) I, e =
+ *      dl sqrt(d)):
+ *        y = S^-1 (x - mu) (asss.py:214, :33-45): y_j = b_j / D_j,
+ *          b_r = fmaf(-U_rj, y_j e_j, b_r)
+ *        av = U (e * v)  (S v_raw = av + eps sqrt(d) v_raw)
+ *        wy = U^-1 y     (wy_j = y_j - ty_j, ty_r = fmaf(U_rj, wy_j, ty_r))
+ *        wv = U^-1 v_raw (wv_j = v_j - tv_j, tv_r = fmaf(U_rj, wv_j, tv_r))
+ *      Since S y = x - mu, S z = 2 (x - mu) / den and S v = (S v_raw - dot
+ *      S z) / |v|; U^-1 z and U^-1 v follow the same way from wy, wv.  The
+ *      round-5 passes B (S z, S v) and C (w = U^-1 delta) are gone: with q =
+ *      (z c + v s) / om at the accepted angle, delta = S q, so U^-1 delta =
+ *      sqrt(d) (dl q + eps U^-1 q) -- the same quantities up to rounding.
  *   the potential along the slice circle: with a = S z, b = S v, g = mu - m,
  *      D(th) = (a c + b s) / om + g and Y(th) = (Pa c + Pb s) / om + Pg, where
  *      Pa, Pb, Pg are fmaf chains over k of P[k][r] (once per transition);
- *      U(th) = 0.5 big_sum(D Y) + c0 -- each shrink step is O(d)
- *   C  w = U^-1 delta (s_r = fmaf(U_rj, w_j, s_r), w_j = delta_j - s_j)
+ *      U(th) = 0.5 big_sum(D Y) + c0 -- each shrink step is O(d).  The stored
+ *      potential is this U at the accepted angle (the model potential of the
+ *      stored x' up to rounding, not re-evaluated at it)
  *   D  the rank-one update as the large-d ARWMH step pass with a_j = q_j -
  *      dl_j, b_j = c_j q_j (no step size), sdiff = sqrt(big_sum(row sums)).
  * Draws as the d <= 64 kernel (Philox(r, i, 0, TAG_ASSS)).  as_change =
@@ -1612,17 +1623,31 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
   const float th0 = 6.28318548f * amh_unif01_from_bits(o0.v[3]);
   /* pass A */
   float e[ORC_BIG], invD[ORC_BIG], b[ORC_BIG], y[ORC_BIG], t[ORC_BIG];
+  float hv[ORC_BIG], av[ORC_BIG], ty[ORC_BIG], tv[ORC_BIG], wy[ORC_BIG], wv[ORC_BIG];
   for (int r = 0; r < d; ++r) {
     e[r] = s->dl[r] * sd;
     invD[r] = 1.0f / ((s->dl[r] + cfg->eps) * sd);
     b[r] = s->z[r] - s->mu[r];
+    hv[r] = e[r] * v[r];
+    av[r] = ty[r] = tv[r] = 0.0f;
   }
   for (int j = 0; j < d; ++j) {
     const float yl = b[j] * invD[j];
     y[j] = yl;
     const float g = yl * e[j];
-    for (int r = j + 1; r < d; ++r) b[r] = fmaf(-s->U[r][j], g, b[r]);
+    av[j] = fmaf(1.0f, hv[j], av[j]);
+    wy[j] = yl - ty[j];
+    wv[j] = v[j] - tv[j];
+    for (int r = j + 1; r < d; ++r) {
+      const float uo = s->U[r][j];
+      b[r] = fmaf(-uo, g, b[r]);
+      av[r] = fmaf(uo, hv[j], av[r]);
+      ty[r] = fmaf(uo, wy[j], ty[r]);
+      tv[r] = fmaf(uo, wv[j], tv[r]);
+    }
   }
+  float svr[ORC_BIG];
+  for (int r = 0; r < d; ++r) svr[r] = av[r] + epsd * v[r]; /* S v_raw */
   for (int r = 0; r < d; ++r) t[r] = y[r] * y[r];
   const float ns = big_sum(t, d);
   const float den = ns + 1.0f;
@@ -1640,25 +1665,13 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
   const int degen = !(nv > 0.0f);
   for (int r = 0; r < d; ++r) v[r] = degen ? 0.0f : v[r] / nv;
   vd = degen ? 0.0f : vd / nv;
-  /* pass B */
-  float a[ORC_BIG], bb[ORC_BIG], hz[ORC_BIG], hv[ORC_BIG];
-  for (int r = 0; r < d; ++r) {
-    hz[r] = e[r] * zr[r];
-    hv[r] = e[r] * v[r];
-    a[r] = bb[r] = 0.0f;
-  }
-  for (int j = 0; j < d; ++j) {
-    a[j] = fmaf(1.0f, hz[j], a[j]);
-    bb[j] = fmaf(1.0f, hv[j], bb[j]);
-    for (int r = j + 1; r < d; ++r) {
-      a[r] = fmaf(s->U[r][j], hz[j], a[r]);
-      bb[r] = fmaf(s->U[r][j], hv[j], bb[r]);
-    }
-  }
   float Sz[ORC_BIG], Sv[ORC_BIG], gm[ORC_BIG], Pa[ORC_BIG], Pb[ORC_BIG], Pg[ORC_BIG];
+  float Wz[ORC_BIG], Wv[ORC_BIG];
   for (int r = 0; r < d; ++r) {
-    Sz[r] = a[r] + epsd * zr[r];
-    Sv[r] = bb[r] + epsd * v[r];
+    Sz[r] = (2.0f * (s->z[r] - s->mu[r])) / den; /* S z = 2 S y / den, S y = x - mu */
+    Sv[r] = degen ? 0.0f : fmaf(-dot, Sz[r], svr[r]) / nv;
+    Wz[r] = (2.0f * wy[r]) / den; /* U^-1 z */
+    Wv[r] = degen ? 0.0f : fmaf(-dot, Wz[r], wv[r]) / nv;
     gm[r] = s->mu[r] - m[r];
     Pa[r] = Pb[r] = Pg[r] = 0.0f;
   }
@@ -1690,10 +1703,14 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
   int iter = 0;
   float ux;
   int cont;
+  float cst, snt, omt; /* the angle of xt */
   {
     float sn, cs, om;
     amh_sincosf(th, &sn, &cs);
     ASSS_BIG_EVAL(cs, sn, xt, om, ux);
+    cst = cs;
+    snt = sn;
+    omt = om;
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
     cont = !degen && ((pt > tpe) || (om < cfg->eps));
@@ -1706,6 +1723,9 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
     float sn, cs, om;
     amh_sincosf(th, &sn, &cs);
     ASSS_BIG_EVAL(cs, sn, xt, om, ux);
+    cst = cs;
+    snt = sn;
+    omt = om;
     float pt = ux + fd * amh_logf(om);
     if (amh_isnan(pt)) pt = INFINITY;
     iter += 1;
@@ -1713,6 +1733,11 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
   }
 #undef ASSS_BIG_EVAL
   const int capped = degen || iter >= 50;
+  if (capped) { /* theta = 0 (asss.py:94) */
+    cst = 1.0f;
+    snt = 0.0f;
+    omt = om0;
+  }
   float xn[ORC_BIG];
   for (int r = 0; r < d; ++r) xn[r] = capped ? x0[r] : xt[r];
   float pen = capped ? U0 : ux;
@@ -1726,7 +1751,7 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
   const int32_t itr = (int32_t)it + 1;
   const int32_t n = ((int32_t)it < cfg->num_warmup) ? itr : itr - cfg->num_warmup;
   const float gamma = amh_lr_gamma(n, cfg->lr_decay);
-  float delta[ORC_BIG], mun[ORC_BIG], Dg[ORC_BIG], one[ORC_BIG], ws[ORC_BIG], sw[ORC_BIG], gw2[ORC_BIG];
+  float delta[ORC_BIG], mun[ORC_BIG], Dg[ORC_BIG], one[ORC_BIG], ws[ORC_BIG], gw2[ORC_BIG];
   float bsc[ORC_BIG], cc[ORC_BIG], qq[ORC_BIG], sacc[ORC_BIG];
   const float sq = sqrtf(1.0f - gamma);
   for (int r = 0; r < d; ++r) {
@@ -1737,13 +1762,13 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
     const float ajj = sq * s->dl[r];
     Dg[r] = ajj * ajj;
     one[r] = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : NAN;
-    sw[r] = 0.0f;
   }
   const float locd = sqrtf(big_sum(t, d));
-  /* pass C */
-  for (int j = 0; j < d; ++j) {
-    ws[j] = delta[j] - sw[j];
-    for (int r = j + 1; r < d; ++r) sw[r] = fmaf(s->U[r][j], ws[j], sw[r]);
+  /* w = U^-1 delta = sqrt(d) (dl q + eps U^-1 q), q = (z c + v s) / om */
+  for (int r = 0; r < d; ++r) {
+    const float q = ((zr[r] * cst) + (v[r] * snt)) / omt;
+    const float wq = ((Wz[r] * cst) + (Wv[r] * snt)) / omt;
+    ws[r] = ((s->dl[r] * q) + (cfg->eps * wq)) * sd;
   }
   for (int r = 0; r < d; ++r) {
     gw2[r] = gamma * (ws[r] * ws[r]);
