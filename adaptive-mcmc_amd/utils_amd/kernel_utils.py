@@ -104,3 +104,10 @@ def get_taus_n_sss(rng_key, kernel, X, adapt_state, n: int = 1, n_samples: int =
     xl = np.tan((phi - e) / np.float32(2)) * sc + loc
     xr = np.tan((phi + e) / np.float32(2)) * sc + loc
     return _taus_from_pairs(kernel, rng_key, np.stack([xl, xr], axis=1).astype(np.float32), adapt_state, n, n_samples)
+
+
+def get_max_taus(rng_key, kernel, X, adapt_state, n_list, n_samples: int = 500000, eps: float = 1e-1) -> list:
+    """Cells 41 / 91 (`get_max_taus`): max over the grid X of
+    get_taus_n_sss(..., n) for every n in n_list (the same rng_key each time)."""
+    return [float(get_taus_n_sss(rng_key, kernel, X, adapt_state, n=n, n_samples=n_samples, eps=eps).max())
+            for n in n_list]

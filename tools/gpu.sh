@@ -28,6 +28,7 @@ mkdir -p $O
 HB=$!
 trap "kill $HB 2>/dev/null" EXIT
 
+NPY=0
 run() {  # run LIMIT LOG cmd...
   local lim=$1 log=$2; shift 2
   timeout -k 10 $lim "$@" > $O/$log 2>&1
@@ -66,7 +67,7 @@ for step in "$@"; do
           rc=$?; echo "$n: $(grep -v amdgpu.ids $O/ab_${n}_$rep.txt | tail -1)"; [ $rc -eq 0 ] || exit $rc
         done
       done ;;
-    py) run 600 py_$(basename ${args%% *} .py).log python3 -u $args ;;
+    py) NPY=$((NPY + 1)); run 600 py${NPY}_$(basename ${args%% *} .py).log python3 -u $args ;;
     rocpy)
       name=${arg%%:*}; rest=${arg#*:}; rest=${rest//+/ }
       run 600 $name.log rocprofv3 --kernel-trace --stats -d $O/$name -o run --output-format csv -- python3 $rest ;;
