@@ -18,7 +18,11 @@
 #   ab:SCRIPT+ARGS   the same A/B for any python tool script
 #   py:SCRIPT+ARGS   one python tool script
 #   rocpy:NAME:SCRIPT+ARGS   rocprofv3 --kernel-trace --stats of a tool script (NAME/)
-#   pmcpy:NAME:SCRIPT+ARGS   FETCH_SIZE / WRITE_SIZE passes of a tool script (NAME_pmc_*/)
+#   pmcpy:NAME:SCRIPT+ARGS   FETCH_SIZE / WRITE_SIZE passes of a tool script (NAME/pmc_*/;
+#                    tools/pooled_pmc_summary.py gpurun_out/TAG/NAME)
+# Summaries: tools/prof_summary.py TAG --src gpurun_out/TAG after `trace pmc`
+# (the step kernel's trace + FETCH/WRITE -> profiles/TAG_step_kernel.json).
+# (The per-round gpu_r*.sh / gpu_ab*.sh scripts of rounds 1-5 are folded in here.)
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 TAG=$1; shift
@@ -74,7 +78,8 @@ for step in "$@"; do
     pmcpy)
       name=${arg%%:*}; rest=${arg#*:}; rest=${rest//+/ }
       for C in FETCH_SIZE WRITE_SIZE; do
-        run 300 ${name}_pmc_$C.log rocprofv3 --pmc $C -d $O/${name}_pmc_$C -o pmc --output-format csv -- python3 $rest
+        mkdir -p $O/$name
+        run 300 ${name}_pmc_$C.log rocprofv3 --pmc $C -d $O/$name/pmc_$C -o pmc --output-format csv -- python3 $rest
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac

@@ -1,11 +1,11 @@
 """HBM traffic of the pooled d = 64 step (configs[4] per GPU) from the two
-rocprofv3 --pmc passes of tools/gpu_pooled_pmc.sh: FETCH_SIZE (KiB; doubled,
+rocprofv3 --pmc passes (tools/gpu.sh pmcpy:NAME:tools/pooled_run.py+...): FETCH_SIZE (KiB; doubled,
 the gfx950 correction for 16-B/lane streaming reads -- the factor and noise
 rows are read that way, MI355X_MICROARCH.md) and WRITE_SIZE (KiB) per launch
 of each pooled kernel, averaged over the last N launches, and the step's
 total against the algorithmic B_B(64) = 2 * 4 * (64 + 3) = 536 B per
 chain-step.
-  python3 tools/pooled_pmc_summary.py gpurun_out/<tag> [--chains 65536] [--last 20] [--k K]"""
+  python3 tools/pooled_pmc_summary.py gpurun_out/<tag>/<name> [--chains 65536] [--last 20] [--k K]"""
 import argparse
 import collections
 import csv

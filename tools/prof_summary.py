@@ -1,4 +1,4 @@
-"""Summarise a tools/gpu_profile.sh run into profiles/<tag>_*.
+"""Summarise a `tools/gpu.sh TAG trace pmc` run into profiles/<tag>_*.
 
 Inputs (gpurun_out/prof_<tag>/): rocprofv3 --kernel-trace --stats of
 `bench.py --steps S --warmup W` and two --pmc passes (FETCH_SIZE,
@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--pmc-warmup", type=int, default=2)
     ap.add_argument("--chains", type=int, default=65536)
     ap.add_argument("--dim", type=int, default=64)
-    ap.add_argument("--src", default=None, help="run directory (default gpurun_out/prof_<tag>; tools/gpu_full.sh "
+    ap.add_argument("--src", default=None, help="run directory (default gpurun_out/prof_<tag>; tools/gpu.sh "
                                                 "writes gpurun_out/<tag>)")
     a = ap.parse_args()
     src = a.src or os.path.join(ROOT, "gpurun_out", f"prof_{a.tag}")
