@@ -893,6 +893,83 @@ __device__ __forceinline__ void s64_sweep1(float& w, float u) {
                "v_fma_f32 %0, -%1, %3, %0\n\ts_mov_b64 exec, %2"
                : "+v"(w), "=&s"(t), "=&s"(sv) : "v"(u), "n"(J), "n"(J + 1));
 }
+// LDS batches read and waited for in ONE statement (outputs "=&v"): per
+// batch one boundary pad instead of two (the separate read and wait
+// statements each had hipcc's pad around them).  AMH_S64_LDSW=0 keeps the
+// separate statements (A/B).
+#ifndef AMH_S64_LDSW
+#define AMH_S64_LDSW 1
+#endif
+template <int O0, int O1>
+__device__ __forceinline__ void lds_ld4x2w(f32x4& a, f32x4& b, uint32_t addr) {
+  asm volatile("ds_read_b128 %0, %2 offset:%3\n\tds_read_b128 %1, %2 offset:%4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a), "=&v"(b)
+               : "v"(addr), "n"(O0), "n"(O1));
+}
+// a, b from addr0 (offsets O0, O1); c, d from addr1 (O2, O3)
+template <int O0, int O1, int O2, int O3>
+__device__ __forceinline__ void lds_ld4x4w(f32x4& a, f32x4& b, f32x4& c, f32x4& d, uint32_t addr0, uint32_t addr1) {
+  asm volatile("ds_read_b128 %0, %4 offset:%6\n\tds_read_b128 %1, %4 offset:%7\n\t"
+               "ds_read_b128 %2, %5 offset:%8\n\tds_read_b128 %3, %5 offset:%9\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a), "=&v"(b), "=&v"(c), "=&v"(d)
+               : "v"(addr0), "v"(addr1), "n"(O0), "n"(O1), "n"(O2), "n"(O3));
+}
+
+// sweep 1 over eight columns J0 .. J0 + 7 (seven when J0 = 56: columns up to
+// 62) in one statement: exec saved once and restored once, each column
+// s_lshl exec (lanes r > J) / v_readlane / s_nop 1 / v_fma / s_nop 0 -- the
+// s_nop 0 is the VALU-write -> v_readlane wait state of the next column (the
+// per-column statements had hipcc's boundary pad there, plus an exec save
+// and restore per column: 8 slots per column, now 5).  The same fma, in the
+// same order, as s64_sweep1.
+#define AMH_SW1_COL(k)                                                          \
+  "s_lshl_b64 exec, -1, %[s" #k "]\n\tv_readlane_b32 %[t], %[w], %[l" #k "]\n\t" \
+  "s_nop 1\n\tv_fma_f32 %[w], -%[t], %[u" #k "], %[w]\n\ts_nop 0\n\t"
+template <int J0>
+__device__ __forceinline__ void s64_sweep1x8(float& w, const float (&U)[64]) {
+  uint64_t sv;
+  uint32_t t;
+  if constexpr (J0 + 7 <= 62) {
+    asm volatile("s_mov_b64 %[sv], exec\n\t" AMH_SW1_COL(0) AMH_SW1_COL(1) AMH_SW1_COL(2) AMH_SW1_COL(3)
+                 AMH_SW1_COL(4) AMH_SW1_COL(5) AMH_SW1_COL(6) AMH_SW1_COL(7) "s_mov_b64 exec, %[sv]"
+                 : [w] "+v"(w), [t] "=&s"(t), [sv] "=&s"(sv)
+                 : [u0] "v"(U[J0]), [u1] "v"(U[J0 + 1]), [u2] "v"(U[J0 + 2]), [u3] "v"(U[J0 + 3]),
+                   [u4] "v"(U[J0 + 4]), [u5] "v"(U[J0 + 5]), [u6] "v"(U[J0 + 6]), [u7] "v"(U[J0 + 7]),
+                   [s0] "n"(J0 + 1), [s1] "n"(J0 + 2), [s2] "n"(J0 + 3), [s3] "n"(J0 + 4), [s4] "n"(J0 + 5),
+                   [s5] "n"(J0 + 6), [s6] "n"(J0 + 7), [s7] "n"(J0 + 8), [l0] "n"(J0), [l1] "n"(J0 + 1),
+                   [l2] "n"(J0 + 2), [l3] "n"(J0 + 3), [l4] "n"(J0 + 4), [l5] "n"(J0 + 5), [l6] "n"(J0 + 6),
+                   [l7] "n"(J0 + 7));
+  } else {
+    static_assert(J0 == 56, "sweep 1 covers columns 0 .. 62");
+    asm volatile("s_mov_b64 %[sv], exec\n\t" AMH_SW1_COL(0) AMH_SW1_COL(1) AMH_SW1_COL(2) AMH_SW1_COL(3)
+                 AMH_SW1_COL(4) AMH_SW1_COL(5) AMH_SW1_COL(6) "s_mov_b64 exec, %[sv]"
+                 : [w] "+v"(w), [t] "=&s"(t), [sv] "=&s"(sv)
+                 : [u0] "v"(U[J0]), [u1] "v"(U[J0 + 1]), [u2] "v"(U[J0 + 2]), [u3] "v"(U[J0 + 3]),
+                   [u4] "v"(U[J0 + 4]), [u5] "v"(U[J0 + 5]), [u6] "v"(U[J0 + 6]), [s0] "n"(J0 + 1),
+                   [s1] "n"(J0 + 2), [s2] "n"(J0 + 3), [s3] "n"(J0 + 4), [s4] "n"(J0 + 5), [s5] "n"(J0 + 6),
+                   [s6] "n"(J0 + 7), [l0] "n"(J0), [l1] "n"(J0 + 1), [l2] "n"(J0 + 2), [l3] "n"(J0 + 3),
+                   [l4] "n"(J0 + 4), [l5] "n"(J0 + 5), [l6] "n"(J0 + 6));
+  }
+}
+#undef AMH_SW1_COL
+#ifndef AMH_S64_SW1_PERCOL
+#define AMH_S64_SW1_PERCOL 0  // 1: the per-column statements (A/B)
+#endif
+// the whole sweep 1 (columns 0 .. 62)
+__device__ __forceinline__ void s64_sweep1_all(float& w, const float (&U)[64]) {
+#if AMH_S64_SW1_PERCOL
+  static_for<63>([&](auto J) {
+    s64_sweep1<J>(w, U[J]);
+    column_fence<J>();
+  });
+#else
+  static_for<8>([&](auto B) {
+    s64_sweep1x8<8 * B>(w, U);
+    __builtin_amdgcn_sched_barrier(0);
+  });
+#endif
+}
+
 // lanes 16Q .. 16Q+15 write v0..v3 at a, a+64, a+128, a+192 (a = scratch + 4 (r mod 16))
 template <int Q>
 __device__ __forceinline__ void s64_wr4_quarter(uint32_t a, float v0, float v1, float v2, float v3) {
@@ -935,15 +1012,19 @@ __device__ __forceinline__ float s64_gauss_pot(float diff, uint32_t x_a, uint32_
     constexpr int b = B;
     constexpr int NQ = kS64PB / 4;
     f32x4 pv[NQ], dv[NQ];
-    static_for<NQ>([&](auto Q) {
-      pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
-      dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
-    });
-    if constexpr (NQ == 4) {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
-                   "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+    if constexpr (NQ == 2 && AMH_S64_LDSW) {
+      lds_ld4x4w<16 * (2 * b), 16 * (2 * b + 1), 16 * (2 * b), 16 * (2 * b + 1)>(pv[0], pv[1], dv[0], dv[1], prow, x_a);
     } else {
-      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+      static_for<NQ>([&](auto Q) {
+        pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
+        dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
+      });
+      if constexpr (NQ == 4) {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
+                     "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+      }
     }
     static_for<2 * NQ>([&](auto K2) {
       const f32x4 q = pv[(int)K2 / 2];
@@ -1026,11 +1107,15 @@ __device__ __forceinline__ void asss_transition64(const StepParams& p, float (&U
     static_for<d / kS64EB>([&](auto B) {
       constexpr int bb = B;
       f32x4 ev[kS64EB / 4];
-      static_for<kS64EB / 4>([&](auto Q) { ev[(int)Q] = lds_ld4<16 * (kS64EB / 4 * bb + Q)>(x_a); });
-      if constexpr (kS64EB == 16) {
-        lds_wait(ev[0], ev[1], ev[2], ev[3]);
+      if constexpr (kS64EB == 8 && AMH_S64_LDSW) {
+        lds_ld4x2w<16 * (2 * bb), 16 * (2 * bb + 1)>(ev[0], ev[1], x_a);
       } else {
-        s64_tie(ev[0], ev[1]);
+        static_for<kS64EB / 4>([&](auto Q) { ev[(int)Q] = lds_ld4<16 * (kS64EB / 4 * bb + Q)>(x_a); });
+        if constexpr (kS64EB == 16) {
+          lds_wait(ev[0], ev[1], ev[2], ev[3]);
+        } else {
+          s64_tie(ev[0], ev[1]);
+        }
       }
       static_for<kS64EB>([&](auto K) {
         constexpr int j = kS64EB * bb + K;
@@ -1112,11 +1197,8 @@ __device__ __forceinline__ void asss_transition64(const StepParams& p, float (&U
   const float ajj = sq * dl;
   const float Dg = ajj * ajj;
   const float one = (amh_isfinite(ajj) && ajj != 0.0f) ? 1.0f : __int_as_float(0x7FC00000);
-  float ws = delta;  // sweep 1: lane r ends with w*_r (s64_sweep1)
-  static_for<d - 1>([&](auto J) {
-    s64_sweep1<J>(ws, U[J]);
-    column_fence<J>();
-  });
+  float ws = delta;  // sweep 1: lane r ends with w*_r (s64_sweep1_all)
+  s64_sweep1_all(ws, U);
   const float gw2 = gamma * (ws * ws);
   const float tsc = gw2 / Dg;
   const float bb = 1.0f + Gp::excl_scan(tsc, r);
@@ -1136,9 +1218,14 @@ __device__ __forceinline__ void asss_transition64(const StepParams& p, float (&U
       constexpr int g = G4;
       if constexpr (g % 4 == 0) s64_wr4_quarter<g / 4>(xq_a, ws, cc, ac, bc);
       constexpr int gq = g % 4;
-      f32x4 cw = lds_ld4<16 * gq>(x_a), cv = lds_ld4<64 + 16 * gq>(x_a);
-      f32x4 ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
+      f32x4 cw, cv, ca, cb;
+#if AMH_S64_LDSW
+      lds_ld4x4w<16 * gq, 64 + 16 * gq, 128 + 16 * gq, 192 + 16 * gq>(cw, cv, ca, cb, x_a, x_a);
+#else
+      cw = lds_ld4<16 * gq>(x_a), cv = lds_ld4<64 + 16 * gq>(x_a);
+      ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
       lds_wait(cw, cv, ca, cb);
+#endif
       static_for<4>([&](auto Q) {
         constexpr int j = 4 * g + Q;
         const float uo = U[j];
@@ -1366,11 +1453,15 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
       static_for<D / kS64EB>([&](auto B) {  // kS64EB columns per batch
         constexpr int b = B;
         f32x4 e[kS64EB / 4];
-        static_for<kS64EB / 4>([&](auto Q) { e[(int)Q] = lds_ld4<16 * (kS64EB / 4 * b + Q)>(x_a); });
-        if constexpr (kS64EB == 16) {
-          lds_wait(e[0], e[1], e[2], e[3]);
+        if constexpr (kS64EB == 8 && AMH_S64_LDSW) {
+          lds_ld4x2w<16 * (2 * b), 16 * (2 * b + 1)>(e[0], e[1], x_a);
         } else {
-          s64_tie(e[0], e[1]);
+          static_for<kS64EB / 4>([&](auto Q) { e[(int)Q] = lds_ld4<16 * (kS64EB / 4 * b + Q)>(x_a); });
+          if constexpr (kS64EB == 16) {
+            lds_wait(e[0], e[1], e[2], e[3]);
+          } else {
+            s64_tie(e[0], e[1]);
+          }
         }
         static_for<kS64EB>([&](auto K) {
           constexpr int j = kS64EB * b + K;
@@ -1391,15 +1482,19 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
           constexpr int b = B;
           constexpr int NQ = kS64PB / 4;
           f32x4 pv[NQ], dv[NQ];
-          static_for<NQ>([&](auto Q) {
-            pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
-            dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
-          });
-          if constexpr (NQ == 4) {
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
-                         "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+          if constexpr (NQ == 2 && AMH_S64_LDSW) {
+            lds_ld4x4w<16 * (2 * b), 16 * (2 * b + 1), 16 * (2 * b), 16 * (2 * b + 1)>(pv[0], pv[1], dv[0], dv[1], prow, x_a);
           } else {
-            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+            static_for<NQ>([&](auto Q) {
+              pv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(prow);
+              dv[(int)Q] = lds_ld4<16 * (NQ * b + Q)>(x_a);
+            });
+            if constexpr (NQ == 4) {
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(pv[2]), "+v"(pv[3]), "+v"(dv[0]),
+                           "+v"(dv[1]), "+v"(dv[2]), "+v"(dv[3]));
+            } else {
+              asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(pv[0]), "+v"(pv[1]), "+v"(dv[0]), "+v"(dv[1]));
+            }
           }
           static_for<2 * NQ>([&](auto K2) {
             const f32x4 q = pv[(int)K2 / 2];
@@ -1448,10 +1543,7 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
 
       // sweep 1 (lanes r > j): afterwards lane r holds w*_r (forward solve U w* = delta)
       float ws = delta;
-      static_for<D - 1>([&](auto J) {
-        s64_sweep1<J>(ws, U[J]);
-        column_fence<J>();
-      });
+      s64_sweep1_all(ws, U);
 
       const float gw2 = gamma * (ws * ws);
       const float tsc = gw2 / Dg;
@@ -1474,9 +1566,14 @@ __global__ __launch_bounds__(WPB * 64) void arwmh_step64_kernel(StepParams p) {
           // the four coefficient vectors of columns 16(g/4) .. +15 (lanes of that quarter write)
           if constexpr (g % 4 == 0) s64_wr4_quarter<g / 4>(xq_a, ws, c, ac, bc);
           constexpr int gq = g % 4;
-          f32x4 cw = lds_ld4<16 * gq>(x_a), cc = lds_ld4<64 + 16 * gq>(x_a);
-          f32x4 ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
+          f32x4 cw, cc, ca, cb;
+#if AMH_S64_LDSW
+          lds_ld4x4w<16 * gq, 64 + 16 * gq, 128 + 16 * gq, 192 + 16 * gq>(cw, cc, ca, cb, x_a, x_a);
+#else
+          cw = lds_ld4<16 * gq>(x_a), cc = lds_ld4<64 + 16 * gq>(x_a);
+          ca = lds_ld4<128 + 16 * gq>(x_a), cb = lds_ld4<192 + 16 * gq>(x_a);
           lds_wait(cw, cc, ca, cb);
+#endif
           static_for<4>([&](auto Q) {
             constexpr int j = 4 * g + Q;
             const float uo = U[j];
