@@ -1,0 +1,30 @@
+"""ARWMH sample() per launch at large d (regime A: per-chain adaptation; the
+step pass chains the next proposal), correlated Gaussian with kappa = 1e4 as
+BASELINE configs[3]: ms per launch over 100 launches after 50 warm-up
+launches (HIP events).  Usage: python3 tools/big_run.py [C] [d]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "adaptive-mcmc_amd"))
+import torch  # noqa: E402
+
+import posteriors as P  # noqa: E402
+from kernels_amd import ARWMH, PRNGKey  # noqa: E402
+
+C = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
+d = int(sys.argv[2]) if len(sys.argv) > 2 else 256
+k = ARWMH(potential_fn=P.correlated_gaussian(d, log10_kappa=4.0), num_chains=C)
+st = k.init(PRNGKey(0), 0, (torch.rand(C, d, device="cuda") * 4 - 2).contiguous(), (), {})
+for _ in range(50):
+    st = k.sample(st, (), {})
+torch.cuda.synchronize()
+a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+a.record()
+for _ in range(100):
+    st = k.sample(st, (), {})
+b.record()
+torch.cuda.synchronize()
+ms = a.elapsed_time(b) / 100
+lib = os.path.basename(os.path.dirname(os.environ.get("AMH_LIB_PATH", "release/x")))
+print(f"arwmh {lib} C={C} d={d}: {ms:.4f} ms per sample(), {C / ms * 1e3:.4g} chain-steps/s", flush=True)
