@@ -30,15 +30,18 @@ namespace amh {
 // relaxed RMW: an agent-scope release would add an L2 write-back
 // (buffer_wbl2) of the whole XCD, whose L2 then holds the noise blocks'
 // dirty rows -- measured 3.1 us from the last slice to the ticket, 0.7 us
-// without (tools/u64_timeline.py, r4p).  The last arriver then acquires at
-// agent scope (buffer_inv: no stale line of an earlier step's sums in its
-// L2) and reads the sums with agent-scope loads -- the write-through form of
-// cdna_hip_programming.md's in-launch counter hand-off.  Diagnostic variant
-// -DAMH_TICKET_ACQREL: the acquire-release RMW instead.
+// without (tools/u64_timeline.py, r4p).  The last arriver reads the sums with
+// agent-scope (sc1) loads only; with sc1 stores drained before every add that
+// is the guide's write-through hand-off, which needs no acquire fence (round
+// 6: the buffer_inv removed, AMH_HANDOFF_FENCE=1 restores it).  Diagnostic
+// variant -DAMH_TICKET_ACQREL: the acquire-release RMW instead.
 #ifdef AMH_TICKET_ACQREL
 #define AMH_TICKET_ORDER __ATOMIC_ACQ_REL
 #else
 #define AMH_TICKET_ORDER __ATOMIC_RELAXED
+#endif
+#ifndef AMH_HANDOFF_FENCE
+#define AMH_HANDOFF_FENCE 0
 #endif
 
 // fused stats kernel, drawn-ahead noise rows loaded early (diagnostic
@@ -1659,7 +1662,13 @@ __global__ __launch_bounds__(512) void pooled_update64_kernel(PooledUpdateParams
     // arriver acquires (AMH_TICKET_ORDER above)
     if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(ticket, 1, AMH_TICKET_ORDER, __HIP_MEMORY_SCOPE_AGENT);
     __syncthreads();
-    if (tk == nred - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // the last arriver: every block's sums
+    // The last arriver reads every block's sums with sc1 (agent-scope relaxed)
+    // loads only, the producers stored them sc1 and drained before their add:
+    // the write-through form that replaces the acquire (MI355X_MICROARCH.md,
+    // inter-workgroup visibility, "Valid forms", first table row), so no
+    // buffer_inv (~1.7 us) sits on the update's critical path.
+    // AMH_HANDOFF_FENCE=1 keeps the acquire (A/B).
+    if (AMH_HANDOFF_FENCE && tk == nred - 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     if (tk != nred - 1) {  // not the last: a noise worker
       if (nlate == 0) {
         URT_FLUSH
@@ -2026,7 +2035,7 @@ __global__ __launch_bounds__(256) void pooled_big_post_kernel(PooledUpdateParams
   }
   __syncthreads();
   if (!last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  if (AMH_HANDOFF_FENCE) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // sc1 loads below (see update64)
   // as_change = sqrtf(big_sum of the column sums)
   const float v = t < d ? __uint_as_float(__hip_atomic_load(&colsum[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
                         : 0.0f;
