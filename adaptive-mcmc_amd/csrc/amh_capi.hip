@@ -3,6 +3,8 @@
 // enqueues the kernels of amh_kernels.hip on the caller's stream.
 #include <hip/hip_runtime.h>
 
+#include <dlfcn.h>
+
 #include <cstdio>
 #include <cstring>
 #include <new>
@@ -878,6 +880,37 @@ int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state*
 int amh_pooled_step(amh_handle* h, int64_t num_chains, const amh_pooled_state* in, const amh_pooled_state* out,
                     int32_t n_steps, double* sums, void* stream) {
   return amh_pooled_step_k(h, num_chains, in, out, n_steps, 1, sums, stream);
+}
+
+// ncclAllReduce / ncclGetErrorString of the RCCL instance already in the
+// process (the caller created `comm` with it: torch's librccl.so.1, found by
+// soname without loading anything), else the system librccl.so.1
+typedef int (*nccl_allreduce_fn)(const void*, void*, size_t, int, int, void*, void*);
+typedef const char* (*nccl_errstr_fn)(int);
+static void* rccl_handle() {
+  static void* hd = nullptr;
+  if (hd == nullptr) {
+    hd = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (hd == nullptr) hd = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (hd == nullptr) hd = dlopen("librccl.so.1", RTLD_NOW);
+  }
+  return hd;
+}
+
+int amh_pooled_allreduce(amh_handle* h, double* sums, int64_t n, void* rccl_comm, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_pooled_allreduce: null handle");
+  if (!sums || !rccl_comm || n < 0) return fail(h, AMH_EINVAL, "amh_pooled_allreduce: null sums / communicator");
+  void* hd = rccl_handle();
+  auto ar = hd ? (nccl_allreduce_fn)dlsym(hd, "ncclAllReduce") : nullptr;
+  if (ar == nullptr) return fail(h, AMH_EHIP, "amh_pooled_allreduce: librccl not found");
+  constexpr int kNcclFloat64 = 8, kNcclSum = 0;
+  const int rc = ar(sums, sums, (size_t)n, kNcclFloat64, kNcclSum, rccl_comm, stream);
+  if (rc != 0) {
+    auto es = (nccl_errstr_fn)dlsym(hd, "ncclGetErrorString");
+    return fail(h, AMH_EHIP, std::string("amh_pooled_allreduce: ncclAllReduce: ") + (es ? es(rc) : "error") +
+                                 " (ncclResult " + std::to_string(rc) + ")");
+  }
+  return AMH_OK;
 }
 
 #ifdef AMH_STAMPS

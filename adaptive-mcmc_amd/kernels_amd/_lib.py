@@ -31,7 +31,7 @@ EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bi
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
-           "amh_normals", "amh_sinkhorn_lse", "amh_check_device")
+           "amh_normals", "amh_sinkhorn_lse", "amh_check_device", "amh_pooled_allreduce")
 
 
 class AmhConfig(ctypes.Structure):
@@ -115,9 +115,10 @@ def lib():
     L.amh_pooled_step.argtypes = [P, I64, PS, PS, I32, P, P]
     L.amh_pooled_stats_k.argtypes = [P, I64, PS, I32, P, P, P, P]
     L.amh_pooled_update_k.argtypes = [P, P, PS, PS, I32, P]
+    L.amh_pooled_allreduce.argtypes = [P, P, I64, P, P]
     L.amh_pooled_step_k.argtypes = [P, I64, PS, PS, I32, I32, P, P]
     for name in ("amh_pooled_sums_size", "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step",
-                 "amh_pooled_stats_k", "amh_pooled_update_k", "amh_pooled_step_k"):
+                 "amh_pooled_stats_k", "amh_pooled_update_k", "amh_pooled_step_k", "amh_pooled_allreduce"):
         getattr(L, name).restype = ctypes.c_int
     L.amh_version.argtypes = []
     for name in EXPORTS[:10]:

@@ -197,9 +197,21 @@ class RcclComm:
             raise RuntimeError("RcclComm is closed")
         return self._ptr
 
-    def all_reduce_sum(self, buf: torch.Tensor, stream=None):
+    def all_reduce_sum(self, buf: torch.Tensor, stream=None, handle=None):
         """In-place all_reduce(sum) of a contiguous device tensor on `stream`
-        (default: the current stream of buf's device)."""
+        (default: the current stream of buf's device).  With a library
+        `handle` (kernels_amd._lib.Handle) and float64 sums the call goes
+        through the C ABI's amh_pooled_allreduce (include/amh.h), the entry a
+        non-Python binding uses; otherwise through ctypes into librccl."""
+        if handle is not None and buf.dtype == torch.float64 and buf.is_cuda and buf.is_contiguous():
+            from . import _lib
+            s = stream if stream is not None else torch.cuda.current_stream(buf.device)
+            L = _lib.lib()
+            rc = L.amh_pooled_allreduce(handle.h, buf.data_ptr(), buf.numel(), self.ptr, s.cuda_stream)
+            if rc != 0:
+                msg = L.amh_last_error(handle.h)
+                raise RcclError(msg.decode() if msg else f"amh_pooled_allreduce: {rc}")
+            return
         rccl_allreduce_sum(buf, self.ptr, stream)
 
     def close(self):

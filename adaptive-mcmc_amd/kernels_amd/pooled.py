@@ -11,8 +11,9 @@ so mu moves by gamma * mean delta, Sigma = L L^T is blended with the mean
 outer product and refactorised (kept if not positive definite), and lambda
 follows the mean acceptance.  With one chain in total this is the
 reference's recurrence.  Across ranks the sums vector (d + d(d+1)/2 + 2
-doubles) is the only exchange: one all-reduce(sum) per step over
-torch.distributed (RCCL over xGMI on MI355X).
+doubles) is the only exchange: one all-reduce(sum) per step (per K steps
+with sync_every = K) over RCCL on xGMI, on this package's own communicator
+(distributed.RcclComm) through the C ABI's amh_pooled_allreduce.
 """
 from __future__ import annotations
 
@@ -53,8 +54,10 @@ class PooledARWMH(ARWMH):
     `sample` advances one block and `sample_(n)` needs n % K == 0;
     num_warmup must be a multiple of K.
 
-    The all-reduce runs on a side stream of its own (RCCL); the compute
-    stream waits on its event only where the sums are consumed.
+    The all-reduce (RCCL, the package's own communicator) is enqueued on the
+    compute stream between the stats and update launches; with overlap it
+    runs on a side stream and the compute stream waits on its event only
+    where the sums are consumed.
 
     overlap = True (the all-reduce overlapped with the next
     proposal) pools with a lag of one block: block b+1 runs with the shared
@@ -183,7 +186,7 @@ class PooledARWMH(ARWMH):
                     warnings.warn(f"RCCL not mapped ({e}); using torch.distributed's stream", RuntimeWarning)
                     self.torch_stream_collective = True
             if self._rccl_comm is not None:
-                self._rccl_comm.all_reduce_sum(buf, torch.cuda.current_stream(dev))
+                self._rccl_comm.all_reduce_sum(buf, torch.cuda.current_stream(dev), handle=self._handle)
                 return None
         if self._comm is None:
             self._comm = torch.cuda.Stream(device=dev)

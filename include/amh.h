@@ -267,6 +267,17 @@ int amh_pooled_step_k(amh_handle* h, int64_t num_chains, const amh_pooled_state*
                       const amh_pooled_state* out, int32_t n_steps, int32_t sync_every, double* sums,
                       void* stream);
 
+/* The exchange between amh_pooled_stats_k and amh_pooled_update_k on N > 1
+ * ranks (SURVEY.md §8(b) amh_pooled_allreduce; no counterpart in the
+ * reference, whose adaptation is per chain): in-place ncclAllReduce(sum) of
+ * the n = amh_pooled_sums_size doubles at `sums` on `stream`, over the
+ * caller's RCCL communicator `rccl_comm` (an ncclComm_t made by
+ * ncclCommInitRank in the same RCCL instance; kernels_amd.distributed.RcclComm
+ * does that).  The RCCL already loaded in the process is used (looked up by
+ * soname), else the system librccl.so.1.  An RCCL error returns AMH_EHIP with
+ * its text in amh_last_error; nothing is retried. */
+int amh_pooled_allreduce(amh_handle* h, double* sums, int64_t n, void* rccl_comm, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -79,6 +79,9 @@ def test_calls_fail_cleanly_without_device(lib):
     bad = lib.AmhConfig(257, 0, 2 / 3, 0.234, 1e-6, (ctypes.c_int32 * 3)(0, 0, 0))
     assert L.amh_create(ctypes.byref(bad), 0, ctypes.byref(h)) == -1
     assert b"dim" in L.amh_last_error(None)
+    # the pooled exchange's entry refuses a null handle / communicator before touching RCCL
+    assert L.amh_pooled_allreduce(None, None, 17, None, None) == -1
+    assert b"amh_pooled_allreduce" in L.amh_last_error(None)
 
 
 def test_product_refuses_cpu_tensors(lib):

@@ -119,7 +119,7 @@ def test_pooled_allreduce_error_propagates(monkeypatch):
         def __init__(self, group, device):
             pass
 
-        def all_reduce_sum(self, buf, stream):
+        def all_reduce_sum(self, buf, stream, handle=None):
             raise D.RcclError("ncclAllReduce: remote process exited (ncclResult 6)")
 
     monkeypatch.setattr(D, "RcclComm", _Comm)
