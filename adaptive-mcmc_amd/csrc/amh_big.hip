@@ -967,6 +967,121 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
   }
 }
 
+// ARWMH.sample_Pnx (arwmh.py:230-270) for the large-d Gaussian: chain c =
+// (point, sample) from x[point] with key split(c), n frozen-theta steps at
+// stream positions 0..n-1 (bit spec: orc_sample_pnx, large d).  The proposal's
+// L xi streams the shared factor column by column (lane l: the fmaf chain of
+// L_rj xi_j over j <= r, rows r = 64 s + l); U(z') takes P's rows in k order
+// (an fmaf chain per row, the MFMA potential's bits) and sums D_r Y_r in the
+// MFMA kernel's tile order (pot_gaussian_big).
+__global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
+  extern __shared__ float lds_big[];
+  const int d = p.d;
+  const int lane = lane_id();
+  const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
+  float* wb0 = lds_big + (size_t)wv * 2 * kColBlk * d;
+  float* wb1 = wb0 + kColBlk * d;
+  const int64_t P = (int64_t)d * (d + 1) / 2;
+  const int64_t nw = (int64_t)gridDim.x * 4;
+  const int64_t C = p.n_points * p.n_samples;
+  const float* m = p.model.data;
+  const float* Pm = p.model.data + d;
+  const float c0 = p.model.data[d + d * d];
+  const float el = amh_expf(p.log_step_size);
+  // U(zz) = 0.5 sum_r D_r Y_r + c0, Y = P D, D = zz - m
+  auto potential = [&](const float (&zz)[kNS]) -> float {
+    float D[kNS], Y[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      const bool act = r < d;
+      D[K] = act ? zz[K] - m[act ? r : 0] : 0.0f;
+      Y[K] = 0.0f;
+    });
+    static_for<kNS>([&](auto KB) {
+      constexpr int kb = KB;
+      if (64 * kb < d) {
+        const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;  // a multiple of 32
+        for (int k2 = 0; k2 < kmax; k2 += 8) {
+          float pr[8][kNS];
+          static_for<8>([&](auto T) {
+            const float* row = Pm + (int64_t)(64 * kb + k2 + T) * d;  // row k = column k (P symmetric)
+            static_for<kNS>([&](auto K) { pr[T][K] = (64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+          });
+          static_for<8>([&](auto T) {
+            const float dk = rdl(D[kb], k2 + T);
+            static_for<kNS>([&](auto K) { Y[K] = fmaf(pr[T][K], dk, Y[K]); });
+          });
+        }
+      }
+    });
+    float q[kNS];
+    static_for<kNS>([&](auto K) { q[K] = (64 * K + lane < d) ? D[K] * Y[K] : 0.0f; });
+    // tile order: 32-row tiles in order, each (ph_0 + ph_1), ph_h the
+    // sequential sum of rows 32 I + (g & 3) + 8 (g >> 2) + 4 h, g = 0..15
+    float S = 0.0f;
+    static_for<kNS>([&](auto K) {
+      static_for<2>([&](auto I2) {
+        if (64 * K + 32 * I2 < d) {
+          float ph[2];
+          static_for<2>([&](auto H) {
+            float a = 0.0f;
+            static_for<16>([&](auto G) {
+              constexpr int l = 32 * I2 + (G & 3) + 8 * (G >> 2) + 4 * H;
+              a = a + rdl(q[K], l);
+            });
+            ph[(int)H] = a;
+          });
+          S = S + (ph[0] + ph[1]);
+        }
+      });
+    });
+    return (0.5f * S) + c0;
+  };
+  for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < C; c += nw) {
+    const int64_t pt = c / p.n_samples;
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, p.key0, p.key1);
+    const uint32_t k0 = kk.v[0], k1 = kk.v[1];
+    float z[kNS];
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      z[K] = (r < d) ? p.x[pt * d + r] : 0.0f;
+    });
+    float pe = potential(z);
+    for (int32_t t = 0; t < p.n; ++t) {
+      float xi[kNS], acc[kNS], zp[kNS];
+      step_noise_rows<kNS>(lane, d, (uint32_t)t, k0, k1, xi);  // bit spec: amh_step_word
+      const float u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)t, k0, k1));  // W_d
+      static_for<kNS>([&](auto K) { acc[K] = 0.0f; });
+      for_columns(p.scale, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+        constexpr int kb = KB;
+        const float xj = rdl(xi[kb], j - 64 * kb);
+        static_for<kNS>([&](auto K) {
+          if constexpr (K >= kb) {
+            const int r = 64 * K + lane;
+            if (r >= j && r < d) acc[K] = fmaf(vv[K], xj, acc[K]);
+          }
+        });
+      });
+      static_for<kNS>([&](auto K) {
+        const bool act = 64 * K + lane < d;
+        zp[K] = act ? z[K] + fmaf(el, acc[K], p.eps * xi[K]) : 0.0f;
+      });
+      float pep = potential(zp);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      if (u < alpha) {  // wave-uniform: one chain per wave
+        static_for<kNS>([&](auto K) { z[K] = zp[K]; });
+        pe = pep;
+      }
+    }
+    static_for<kNS>([&](auto K) {
+      const int r = 64 * K + lane;
+      if (r < d) p.out[c * d + r] = z[K];
+    });
+  }
+}
+
 // ------------------------------------------------------------- launchers ----
 bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256 && d % 32 == 0; }
 // pooled mode: the MFMA path also takes d = 64 (every per-chain product is a
@@ -1000,6 +1115,10 @@ hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
 }
 hipError_t run_asss_big_step(const StepParams& p, hipStream_t s) {
   hipLaunchKernelGGL(asss_big_step_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  return hipGetLastError();
+}
+hipError_t run_big_pnx(const PnxParams& p, hipStream_t s) {
+  hipLaunchKernelGGL(big_pnx_kernel, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s) {

@@ -438,7 +438,8 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_sample_pnx: no model bound");
   if (!key || !x || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
     return fail(h, AMH_EINVAL, "amh_sample_pnx: bad arguments");
-  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 not supported");
+  if (h->cfg.dim > 64 && !amh::big_model(h->model_id, h->cfg.dim))
+    return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 needs the dense Gaussian with d % 32 == 0 up to 256");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
   amh::PnxParams p{};
@@ -454,7 +455,7 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
   p.key1 = key[1];
   p.out = out;
   p.model = h->model;
-  e = amh::run_pnx(h->model_id, p, (hipStream_t)stream);
+  e = (p.d > 64) ? amh::run_big_pnx(p, (hipStream_t)stream) : amh::run_pnx(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx");
   return AMH_OK;
 }

@@ -225,6 +225,8 @@ hipError_t run_big_potential(const PotParams& p, hipStream_t s);
 // ASSS for the large-d Gaussian (big_model): one transition per launch; the
 // frozen kernel of sample_Pnx
 hipError_t run_asss_big_step(const StepParams& p, hipStream_t s);
+// ARWMH.sample_Pnx for the large-d Gaussian (big_model)
+hipError_t run_big_pnx(const PnxParams& p, hipStream_t s);
 hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s);
 
 // split path for data-heavy models (diamonds): proposal kernel, lane-per-chain

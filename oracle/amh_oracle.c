@@ -592,11 +592,21 @@ void orc_split_keys(const uint32_t* key, int64_t n, uint32_t* out) {
   }
 }
 
+static void orc_sample_pnx_big(const orc_cfg* cfg, const uint32_t* keys, const float* x, int64_t n_points,
+                               int64_t n_samples, const float* Lpacked, float log_step_size, int32_t n, float* out);
+
 void orc_sample_pnx(const orc_cfg* cfg, const uint32_t* key, const float* x, int64_t n_points,
                     int64_t n_samples, const float* loc, const float* Lpacked, float log_step_size,
                     int32_t n, float* out) {
   const int d = cfg->d;
   const int64_t C = n_points * n_samples;
+  if (d > ORC_DMAX) {
+    uint32_t* bkeys = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)C);
+    orc_split_keys(key, C, bkeys);
+    orc_sample_pnx_big(cfg, bkeys, x, n_points, n_samples, Lpacked, log_step_size, n, out);
+    free(bkeys);
+    return;
+  }
   uint32_t* keys = (uint32_t*)malloc(sizeof(uint32_t) * 2 * (size_t)C);
   orc_split_keys(key, C, keys);
   (void)loc;
@@ -1127,6 +1137,44 @@ static void orc_step_big(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t
     }
     if (accept_count) accept_count[c] += nacc;
     free(s);
+  }
+}
+
+/* arwmh.py:230-270 (ARWMH.sample_Pnx) for 64 < d <= 256, dense Gaussian,
+ * mirror of big_pnx_kernel (amh_big.hip): the d <= 64 rule (above) with
+ * acc_r the fmaf chain of L_rj xi_j over j <= r (the zero terms j > r of the
+ * small-d loop leave acc unchanged: acc starts at +0 and an fmaf with a zero
+ * product never makes it -0) and U by pot_gaussian_big, the start point's
+ * included. */
+static void orc_sample_pnx_big(const orc_cfg* cfg, const uint32_t* keys, const float* x, int64_t n_points,
+                               int64_t n_samples, const float* Lpacked, float log_step_size, int32_t n, float* out) {
+  const int d = cfg->d;
+  const int64_t C = n_points * n_samples;
+  const float el = amh_expf(log_step_size);
+#pragma omp parallel for schedule(dynamic, 4)
+  for (int64_t c = 0; c < C; ++c) {
+    const int64_t p = c / n_samples;
+    float z[ORC_BIG], zp[ORC_BIG], xi[ORC_BIG];
+    for (int r = 0; r < d; ++r) z[r] = x[p * d + r];
+    float pe = pot_gaussian_big(cfg, z);
+    for (int32_t t = 0; t < n; ++t) {
+      float u = 0.0f;
+      amh_step_noise(d, (uint32_t)t, keys[2 * c], keys[2 * c + 1], xi, &u);
+      for (int r = 0; r < d; ++r) {
+        float acc = 0.0f;
+        for (int j = 0; j <= r; ++j) acc = fmaf(Lpacked[col_off(d, j) + (r - j)], xi[j], acc);
+        zp[r] = z[r] + fmaf(el, acc, cfg->eps * xi[r]);
+      }
+      float pep = pot_gaussian_big(cfg, zp);
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      if (u < alpha) {
+        for (int r = 0; r < d; ++r) z[r] = zp[r];
+        pe = pep;
+      }
+    }
+    for (int r = 0; r < d; ++r) out[c * d + r] = z[r];
   }
 }
 

@@ -148,6 +148,28 @@ def test_sample_pnx_bitexact(gpu, orc):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
+@pytest.mark.parametrize("d", [96, 128, 256])
+def test_sample_pnx_large_d_bitexact(d, gpu, orc):
+    """ARWMH.sample_Pnx at 64 < d <= 256 (big_pnx_kernel: the shared factor
+    streamed per step, U by P's rows in the MFMA potential's order) against
+    orc_sample_pnx's large-d mirror, bit for bit; the adapted state of a
+    short run as the frozen theta, and the start point's potential included."""
+    from kernels_amd import PRNGKey
+    k, st, om, ost = _init("gaussian", 16, gpu, orc, d=d)
+    st = k.sample_(st, 12)
+    ad = st.adapt_state
+    loc = ad.loc[5].cpu().numpy()
+    scale = ad.scale[5].cpu().numpy()
+    lam = float(ad.log_step_size[5].cpu())
+    x = st.z[:3].cpu().numpy()
+    out = k.sample_Pnx(PRNGKey(7), x, (ad.loc[5], ad.scale[5], ad.log_step_size[5]), n=5, n_samples=13)
+    ref = orc.sample_pnx(om, PRNGKey(7), x, loc, scale, lam, 5, 13)
+    assert out.shape == (3, 13, d)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    moved = np.mean(np.any(ref != x[:, None, :], axis=-1))
+    assert moved > 0.2  # the comparison covers accepted moves, not only rejections
+
+
 def test_headline_size_properties(gpu):
     """65,536 chains x d = 64 (BASELINE config 2): after 200 steps every factor
     has a positive finite diagonal, acceptance moves toward 0.234, and the
