@@ -1,5 +1,5 @@
-// amh_big.hip -- ARWMH for large dimensions (64 < d <= 256, d % 32 == 0,
-// dense Gaussian potential; BASELINE config 4: d = 256, kappa = 1e4).
+// amh_big.hip -- ARWMH for large dimensions (64 < d <= 256, dense Gaussian
+// potential; BASELINE config 4: d = 256, kappa = 1e4).
 //
 // At d = 256 a chain's packed factor is 131.6 KB: it cannot live in one
 // wave's registers, and the dense precision (256 KB) cannot sit in LDS next
@@ -61,12 +61,15 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 
 // Column stream of one chain's packed factor (column-major, column j at
 // col_off(d, j)): blocks of 8 columns are contiguous in HBM (and 16-B aligned
-// for d % 32 == 0), so each block is one bulk LDS-DMA of dwordx4 pieces into
-// the wave's double buffer while the previous block is consumed.  LDS reads
+// for d % 8 == 0: col_off(d, 8b) and d (d + 1) / 2 are multiples of 4), so
+// each block is one bulk LDS-DMA of dwordx4 pieces -- dword pieces for other
+// d -- into the wave's double buffer while the previous block is consumed; a
+// ragged last block holds d % 8 columns.  LDS reads
 // go through asm (lds_ld1) so the compiler's wait-count pass does not drain
 // the in-flight DMA before them (see amh_device.h).
 constexpr int kColBlk = 8;
 
+template <bool RAG>
 __device__ __forceinline__ void issue_block(const float* Lc, int d, int64_t P, int b, float* wbuf, int lane) {
   const int j0 = kColBlk * b;
   const int j1 = j0 + kColBlk;
@@ -74,20 +77,27 @@ __device__ __forceinline__ void issue_block(const float* Lc, int d, int64_t P, i
   const int64_t o1 = (j1 < d) ? col_off(d, j1) : P;
   const uint32_t bytes = (uint32_t)(o1 - o0) * 4u;
   const Buf rb(uniform_ptr(Lc + o0), bytes);
-  for (uint32_t o = 0; o < bytes; o += 1024u) {
-    if (o + 16u * (uint32_t)lane < bytes)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rb.rs, (lds_void_t*)(wbuf + o / 4u), 16, (int)(o + 16u * lane), 0, 0, 0);
+  if constexpr (!RAG) {
+    for (uint32_t o = 0; o < bytes; o += 1024u) {
+      if (o + 16u * (uint32_t)lane < bytes)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb.rs, (lds_void_t*)(wbuf + o / 4u), 16, (int)(o + 16u * lane), 0, 0, 0);
+    }
+  } else {
+    for (uint32_t o = 0; o < bytes; o += 256u) {
+      if (o + 4u * (uint32_t)lane < bytes)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rb.rs, (lds_void_t*)(wbuf + o / 4u), 4, (int)(o + 4u * lane), 0, 0, 0);
+    }
   }
 }
 
 // f(KB, j, v) for every column j in order, v[K] = L_rj for rows r = 64 K + l
 // (only rows j < r < d are meaningful; the diagonal L_jj is v[j / 64] of
 // lane j % 64).  KB = j / 64 is a compile-time slot index.
-template <class F>
+template <bool RAG, class F>
 __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, float* wb0, float* wb1, int lane,
                                             F&& f) {
-  const int nb = d / kColBlk;
-  issue_block(Lc, d, P, 0, wb0, lane);
+  const int nb = (d + kColBlk - 1) / kColBlk;
+  issue_block<RAG>(Lc, d, P, 0, wb0, lane);
   static_for<kNS>([&](auto KB) {
     constexpr int kb = KB;
     if (64 * kb < d) {
@@ -97,7 +107,7 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): block b has landed
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): reads of the other buffer done
         float* cur = (b & 1) ? wb1 : wb0;
-        if (b + 1 < nb) issue_block(Lc, d, P, b + 1, (b & 1) ? wb0 : wb1, lane);
+        if (b + 1 < nb) issue_block<RAG>(Lc, d, P, b + 1, (b & 1) ? wb0 : wb1, lane);
         const int64_t ob = col_off(d, kColBlk * b);
         // element (r, j) sits at cur[col_off(d, j) - ob + r - j]; column q + 1's
         // reads are issued before f runs on column q (one LDS round trip off
@@ -118,14 +128,18 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         float vn[kNS];
         rd(0, vn);
         lds_wait(vn[0], vn[1], vn[2], vn[3]);
-        for (int q = 0; q < kColBlk; ++q) {
+        // RAG (d % 8 != 0): a run-time column count for the ragged last
+        // block; the aligned instantiation keeps the compile-time trip count
+        // (a run-time bound in it cost 12-17 % at d = 256)
+        const int qn = RAG ? ((d - kColBlk * b) < kColBlk ? (d - kColBlk * b) : kColBlk) : kColBlk;
+        for (int q = 0; q < qn; ++q) {
           float v[kNS];
           static_for<kNS>([&](auto K) { v[K] = vn[K]; });
 #if AMH_BIG_NOPIPE
           f(KB, kColBlk * b + q, v);
-          if (q + 1 < kColBlk) rd(q + 1, vn);
+          if (q + 1 < qn) rd(q + 1, vn);
 #else
-          if (q + 1 < kColBlk) rd(q + 1, vn);
+          if (q + 1 < qn) rd(q + 1, vn);
           f(KB, kColBlk * b + q, v);
 #endif
           lds_wait(vn[0], vn[1], vn[2], vn[3]);
@@ -183,6 +197,7 @@ __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
 }
 
 // ------------------------------------------------------------- propose ----
+template <bool RAG>
 __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -211,7 +226,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
       mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
       acc[K] = sa[K] = sr[K] = zp[K] = wa[K] = wr[K] = 0.0f;
     });
-    for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+    for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
       constexpr int kb = KB;
       const int jl = j - 64 * kb;
       const float etaj = rdl(eta[kb], jl);
@@ -255,7 +270,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
 // big_propose_kernel on the stored values), so a multi-step launch reads the
 // factor once per transition.  The wave's own xprop / wa / wr rows were read
 // at the top of its chain, so the next ones overwrite them in place.
-template <bool NEXT>
+template <bool NEXT, bool RAG>
 __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -378,7 +393,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
         bc[K] = (cc[K] * qq[K]) * e1;
         sv[K] = 0.0f;
       });
-      for_columns(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+      for_columns<RAG>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       // factor kept (arwmh.py:191): copied verbatim; as_change = ||L (e1 - e0)||_F
       float ac[kNS];
       static_for<kNS>([&](auto K) { ac[K] = (dl[K] * e1) - (dl[K] * el); });
-      for_columns(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+      for_columns<RAG>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float acj = rdl(ac[kb], jl), invj = rdl(inv[kb], jl);
@@ -468,20 +483,26 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
 // ------------------------------------------------- potential on MFMA ----
 // 64 chains per block (two 32-chain tiles), 4 waves; wave w owns the 32-row
 // tiles 2w and 2w + 1.  D = z' - m is staged k-major in LDS ([k][chain],
-// rows padded to 65 floats); A = P rows straight from L2.
+// rows padded to 65 floats); A = P rows straight from L2.  For d % 32 != 0
+// the last tile and the k steps past d see zeros (A and the LDS rows d ..
+// 32 nt - 1): an fmaf with a zero product leaves a sum that started at +0
+// unchanged, so the bits are the k < d chain's.
 constexpr int kPotChains = 64;
 constexpr int kPotLd = 65;
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
-__host__ __device__ inline size_t pot_mfma_lds(int d) { return ((size_t)d * kPotLd + 8 * kPotChains) * sizeof(float); }
+__host__ __device__ inline int pot_rows(int d) { return (d + 31) & ~31; }
+__host__ __device__ inline size_t pot_mfma_lds(int d) { return ((size_t)pot_rows(d) * kPotLd + 8 * kPotChains) * sizeof(float); }
 
+template <bool PAD>  // d % 32 != 0: the zero rows / k steps past d
 __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
   extern __shared__ float lds_pot[];
   const int d = p.d;
   float* Dt = lds_pot;
-  float(*tsum)[kPotChains] = (float(*)[kPotChains])(lds_pot + (size_t)d * kPotLd);
-  const int nt = d / 32;
+  const int dp = pot_rows(d);
+  float(*tsum)[kPotChains] = (float(*)[kPotChains])(lds_pot + (size_t)dp * kPotLd);
+  const int nt = dp / 32;
   const float* m = p.model.data;
   const float* Pm = p.model.data + d;
   const float c0 = p.model.data[d + d * d];
@@ -492,6 +513,12 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
     if (ch >= p.n) ch = p.n - 1;
     Dt[k * kPotLd + cc] = p.z[ch * d + k] - m[k];
   }
+  if constexpr (PAD) {
+    for (int idx = threadIdx.x; idx < kPotChains * (dp - d); idx += 256) {
+      const int cc = idx % kPotChains, k = d + idx / kPotChains;
+      Dt[k * kPotLd + cc] = 0.0f;
+    }
+  }
   __syncthreads();
   const int lane = lane_id();
   const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x / 64));
@@ -500,8 +527,9 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
   static_for<2>([&](auto I) { static_for<2>([&](auto T) { acc[I][T] = f32x16{}; }); });
   const bool has1 = 2 * w + 1 < nt;
   const bool has0 = 2 * w < nt;
-  const float* prow0 = Pm + (int64_t)(32 * (2 * w) + i) * d;
-  const float* prow1 = Pm + (int64_t)(32 * (2 * w + 1) + i) * d;
+  const bool in0 = !PAD || 32 * (2 * w) + i < d, in1 = !PAD || 32 * (2 * w + 1) + i < d;  // rows of P (else zero)
+  const float* prow0 = Pm + (int64_t)(in0 ? 32 * (2 * w) + i : 0) * d;
+  const float* prow1 = Pm + (int64_t)(in1 ? 32 * (2 * w + 1) + i : 0) * d;
   // A operands (P rows, L2) in batches of 8 k-steps, the next batch loaded
   // while the current one feeds the MFMAs
   if (has0) {
@@ -509,8 +537,14 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
     float an0[NB], an1[NB];
     auto load = [&](int kk0) {
       static_for<NB>([&](auto S) {
-        an0[S] = prow0[kk0 + 2 * S + h];
-        an1[S] = has1 ? prow1[kk0 + 2 * S + h] : 0.0f;
+        const int k = kk0 + 2 * S + h;
+        if constexpr (PAD) {
+          an0[S] = (in0 && k < d) ? prow0[k] : 0.0f;
+          an1[S] = (has1 && in1 && k < d) ? prow1[k] : 0.0f;
+        } else {
+          an0[S] = prow0[k];
+          an1[S] = has1 ? prow1[k] : 0.0f;
+        }
       });
     };
     load(0);
@@ -560,7 +594,7 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
 }
 
 // ------------------------------------------------------------------ ASSS ----
-// ASSS (asss.py:192-269) for 64 < d <= 256, d % 32 == 0, dense Gaussian:
+// ASSS (asss.py:192-269) for 64 < d <= 256, dense Gaussian:
 // one wave per chain, lane l owns rows 64 s + l, the factor streamed column
 // by column through the wave's LDS double buffer (for_columns).  Two passes
 // over the factor per transition (bit spec: oracle asss_step_big1; round 5
@@ -581,7 +615,7 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
 // ADAPT = false is the frozen kernel of sample_Pnx (shared loc / factor).
 namespace {
 
-template <bool ADAPT>
+template <bool ADAPT, bool RAG>
 __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, const float (&dl)[kNS],
                                                const float (&inv)[kNS], float (&x)[kNS], float (&mu)[kNS],
                                                float& pe, float& asc, int32_t it, uint32_t k0, uint32_t k1, int d,
@@ -615,7 +649,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     y[K] = av[K] = ty[K] = tv[K] = wy[K] = wv[K] = 0.0f;
   });
 #if !AMH_ABL_NOPASSA
-  for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+  for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
     constexpr int kb = KB;
     const int jl = j - 64 * kb;
     const float yl = rdl(b[kb] * invD[kb], jl);
@@ -686,12 +720,13 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   static_for<kNS>([&](auto KB) {
     constexpr int kb = KB;
     if (64 * kb < d) {
-      const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;  // a multiple of 32
+      const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;
       for (int k2 = 0; k2 < kmax; k2 += 8) {
-        float pr[8][kNS];
+        float pr[8][kNS];  // rows k >= d read as zeros (their terms leave the chains unchanged)
         static_for<8>([&](auto T) {
-          const float* row = Pm + (int64_t)(64 * kb + k2 + T) * d;
-          static_for<kNS>([&](auto K) { pr[T][K] = (64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+          const bool kin = !RAG || k2 + T < kmax;  // d % 8 == 0: kmax is a multiple of 8
+          const float* row = Pm + (int64_t)(kin ? 64 * kb + k2 + T : 0) * d;
+          static_for<kNS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
         });
         static_for<8>([&](auto T) {
           const int kl = k2 + T;
@@ -825,7 +860,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
         bc[K] = cc[K] * qq[K];
         sv[K] = sacc[K] = 0.0f;
       });
-      for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
@@ -853,7 +888,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       });
       sdiff = sqrtf(big_sum(sacc));
     } else if (Lout != Lc && !AMH_ABL_NOPASSD) {  // factor kept (asss.py:255): copied verbatim
-      for_columns(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
         constexpr int kb = KB;
         float* ocol = Lout + col_off(d, j) - j;
         static_for<kNS>([&](auto K) {
@@ -876,6 +911,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
 }  // namespace
 
 // ASSS.sample: one transition of every chain per launch (host loops n_steps)
+template <bool RAG>
 __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -905,7 +941,7 @@ __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
     const float gamma = (n < p.gamma_tab_n) ? ((const cf*)p.gamma_tab)[n] : amh_lr_gamma(n, p.a);
     float pe = p.in.potential_energy[c];
     float asc = 0.0f;
-    asss_big_chain<true>(Lc, Lo, dl, inv, x, mu, pe, asc, it, k0, k1, d, P, p.eps, p.W, gamma, p.model, wb0, wb1,
+    asss_big_chain<true, RAG>(Lc, Lo, dl, inv, x, mu, pe, asc, it, k0, k1, d, P, p.eps, p.W, gamma, p.model, wb0, wb1,
                          lane);
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
@@ -929,6 +965,7 @@ __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
 // ASSS.sample_Pnx: chain c = (point, sample) from x[point] with key split(c),
 // n frozen transitions with the shared (loc, factor), the transition's
 // stream position the step index
+template <bool RAG>
 __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -958,7 +995,7 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
     });
     float pe = 0.0f, asc = 0.0f;
     for (int32_t t = 0; t < p.n; ++t)
-      asss_big_chain<false>(p.scale, nullptr, dl, inv, x, mu, pe, asc, t, kk.v[0], kk.v[1], d, P, p.eps, 0, 0.0f,
+      asss_big_chain<false, RAG>(p.scale, nullptr, dl, inv, x, mu, pe, asc, t, kk.v[0], kk.v[1], d, P, p.eps, 0, 0.0f,
                             p.model, wb0, wb1, lane);
     static_for<kNS>([&](auto K) {
       const int r = 64 * K + lane;
@@ -974,6 +1011,7 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
 // L_rj xi_j over j <= r, rows r = 64 s + l); U(z') takes P's rows in k order
 // (an fmaf chain per row, the MFMA potential's bits) and sums D_r Y_r in the
 // MFMA kernel's tile order (pot_gaussian_big).
+template <bool RAG>
 __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -1000,12 +1038,13 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
     static_for<kNS>([&](auto KB) {
       constexpr int kb = KB;
       if (64 * kb < d) {
-        const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;  // a multiple of 32
+        const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;
         for (int k2 = 0; k2 < kmax; k2 += 8) {
-          float pr[8][kNS];
+          float pr[8][kNS];  // rows k >= d read as zeros
           static_for<8>([&](auto T) {
-            const float* row = Pm + (int64_t)(64 * kb + k2 + T) * d;  // row k = column k (P symmetric)
-            static_for<kNS>([&](auto K) { pr[T][K] = (64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+            const bool kin = !RAG || k2 + T < kmax;  // d % 8 == 0: kmax is a multiple of 8
+            const float* row = Pm + (int64_t)(kin ? 64 * kb + k2 + T : 0) * d;  // row k = column k (P symmetric)
+            static_for<kNS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
           });
           static_for<8>([&](auto T) {
             const float dk = rdl(D[kb], k2 + T);
@@ -1052,7 +1091,7 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
       step_noise_rows<kNS>(lane, d, (uint32_t)t, k0, k1, xi);  // bit spec: amh_step_word
       const float u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)t, k0, k1));  // W_d
       static_for<kNS>([&](auto K) { acc[K] = 0.0f; });
-      for_columns(p.scale, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      for_columns<RAG>(p.scale, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
         constexpr int kb = KB;
         const float xj = rdl(xi[kb], j - 64 * kb);
         static_for<kNS>([&](auto K) {
@@ -1083,7 +1122,7 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
 }
 
 // ------------------------------------------------------------- launchers ----
-bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256 && d % 32 == 0; }
+bool big_model(int model_id, int d) { return model_id == AMH_MODEL_GAUSSIAN && d > 64 && d <= 256; }
 // pooled mode: the MFMA path also takes d = 64 (every per-chain product is a
 // GEMM over chains once the factor is shared)
 bool pooled_big_model(int model_id, int d) {
@@ -1102,32 +1141,39 @@ hipError_t run_big_init(const InitParams& p, hipStream_t s) {
 }
 static size_t stream_lds(int d) { return (size_t)4 * 2 * kColBlk * d * sizeof(float); }
 hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_propose_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
-  return hipGetLastError();
-}
-hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
-  if (next) {
-    hipLaunchKernelGGL(big_step_kernel<true>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  if (p.d % kColBlk) {
+    hipLaunchKernelGGL(big_propose_kernel<true>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   } else {
-    hipLaunchKernelGGL(big_step_kernel<false>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+    hipLaunchKernelGGL(big_propose_kernel<false>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   }
   return hipGetLastError();
 }
+hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
+  const bool rag = p.d % kColBlk != 0;
+  auto k = next ? (rag ? big_step_kernel<true, true> : big_step_kernel<true, false>)
+                : (rag ? big_step_kernel<false, true> : big_step_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  return hipGetLastError();
+}
 hipError_t run_asss_big_step(const StepParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(asss_big_step_kernel, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
+  auto k = (p.d % kColBlk) ? asss_big_step_kernel<true> : asss_big_step_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_pnx(const PnxParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_pnx_kernel, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
+  auto k = (p.d % kColBlk) ? big_pnx_kernel<true> : big_pnx_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(asss_big_pnx_kernel, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
+  auto k = (p.d % kColBlk) ? asss_big_pnx_kernel<true> : asss_big_pnx_kernel<false>;
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_potential(const PotParams& p, hipStream_t s) {
   const int64_t blocks = (p.n + kPotChains - 1) / kPotChains;
-  hipLaunchKernelGGL(gauss_pot_mfma_kernel, dim3((unsigned)blocks), dim3(256), pot_mfma_lds(p.d), s, p);
+  auto k = (p.d % 32) ? gauss_pot_mfma_kernel<true> : gauss_pot_mfma_kernel<false>;
+  hipLaunchKernelGGL(k, dim3((unsigned)blocks), dim3(256), pot_mfma_lds(p.d), s, p);
   return hipGetLastError();
 }
 

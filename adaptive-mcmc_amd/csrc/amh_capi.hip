@@ -212,7 +212,7 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
     return fail(h, AMH_EINVAL, "amh_bind_model: model dimension " + std::to_string(dm) + " != config dim " +
                                    std::to_string(h->cfg.dim));
   if (dm > 64 && !amh::big_model(model_id, dm))
-    return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model with d a multiple of 32 (<= 256)");
+    return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model (d <= 256)");
   // the handle's device for everything below (the caller -- Handle.bind_model --
   // holds it current and restores its own afterwards)
   hipError_t e = hipSetDevice(h->device);
@@ -439,7 +439,7 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
   if (!key || !x || !scale_packed || !out || n_points < 1 || n_samples < 1 || n < 0)
     return fail(h, AMH_EINVAL, "amh_sample_pnx: bad arguments");
   if (h->cfg.dim > 64 && !amh::big_model(h->model_id, h->cfg.dim))
-    return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 needs the dense Gaussian with d % 32 == 0 up to 256");
+    return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 needs the dense Gaussian (d <= 256)");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
   amh::PnxParams p{};
@@ -480,7 +480,7 @@ int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const 
     return fail(h, AMH_EINVAL, "amh_asss_step: bad arguments");
   const bool big = amh::big_model(h->model_id, h->cfg.dim);
   if (h->cfg.dim > 64 && !big)
-    return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64, or a dense Gaussian with d % 32 == 0 up to 256");
+    return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64, or a dense Gaussian up to 256");
   if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_asss_step: thinning must be >= 1");
   if (n_steps == 0) return AMH_OK;
   hipError_t e = hipSetDevice(h->device);
@@ -532,7 +532,7 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
     return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: bad arguments");
   const bool big = amh::big_model(h->model_id, h->cfg.dim);
   if (h->cfg.dim > 64 && !big)
-    return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64, or a dense Gaussian with d % 32 == 0 up to 256");
+    return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64, or a dense Gaussian up to 256");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx/hipSetDevice");
   amh::AsssPnxParams p{};
@@ -657,6 +657,7 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_stats/hipSetDevice");
   const int d = h->cfg.dim;
   const bool big = amh::pooled_big_model(h->model_id, d);
+  if (d > 64 && !big) return fail(h, AMH_EINVAL, "amh_pooled_stats: d > 64 needs d % 32 == 0 in the pooled mode");
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
   const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains, d) : (num_chains + chunk - 1) / chunk;
@@ -795,6 +796,8 @@ static int pooled_update_impl(amh_handle* h, const double* sums, const amh_poole
   if (!sums || !pooled_ok(in) || !pooled_ok(out)) return fail(h, AMH_EINVAL, "amh_pooled_update: bad arguments");
   if (k_steps < 1 || h->cfg.num_warmup % k_steps != 0)
     return fail(h, AMH_EINVAL, "amh_pooled_update: k_steps must be >= 1 and divide num_warmup");
+  if (h->cfg.dim > 64 && !amh::pooled_big_model(h->model_id, h->cfg.dim))
+    return fail(h, AMH_EINVAL, "amh_pooled_update: d > 64 needs d % 32 == 0 in the pooled mode");
   if (int rc = check_device_flag(h)) return rc;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_pooled_update/hipSetDevice");

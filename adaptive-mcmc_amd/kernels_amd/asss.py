@@ -99,15 +99,15 @@ class ASSS(ARWMH):
             raise ValueError("Valid value of `init_params` must be provided with `potential_fn`.")
         st = super().init(rng_key, num_warmup, init_params, model_args, model_kwargs)
         if self._dim > 64 and not self._big_ok():
-            raise ValueError("ASSS supports d <= 64, or the dense Gaussian with d % 32 == 0 up to d = 256")
+            raise ValueError("ASSS supports d <= 64, or the dense Gaussian up to d = 256")
         return self._to_asss(st)
 
     def _big_ok(self) -> bool:
         """64 < d <= 256: the large-d kernel (amh_big.hip asss_big_step_kernel)
-        takes the dense Gaussian with d a multiple of 32 (the reference has no
-        dimension limit, asss.py:192-269)."""
+        takes the dense Gaussian at any such d (the reference has no dimension
+        limit, asss.py:192-269; other models stop at d = 64)."""
         mid = self._model.model_id if self._model is not None else getattr(self._potential_fn, "model_id", None)
-        return mid == _lib.AMH_MODEL_GAUSSIAN and self._dim % 32 == 0 and self._dim <= 256
+        return mid == _lib.AMH_MODEL_GAUSSIAN and self._dim <= 256
 
     def sample(self, state, model_args=(), model_kwargs=None):
         """asss.py:191-258: one transition of every chain; returns a new state."""

@@ -70,9 +70,9 @@ enum {
 
 typedef struct amh_config {
   int32_t dim;                /* d, flat unconstrained dimension: 1..64 for
-                                 every model; 64 < d <= 256 (d % 32 == 0) for
-                                 the Gaussian (regime A and pooled mode);
-                                 ASSS d <= 64 */
+                                 every model; 64 < d <= 256 for the dense
+                                 Gaussian (regime A, sample_Pnx and ASSS; the
+                                 pooled mode needs d % 32 == 0) */
   int32_t num_warmup;         /* W (ARWMH.init's num_warmup)                 */
   float lr_decay;             /* a: gamma_n = 1 / n^a          (default 2/3) */
   float target_accept_prob;   /*                               (default .234)*/

@@ -921,11 +921,12 @@ int orc_pooled_update(const orc_cfg* cfg, const double* sums, int32_t* i_, float
 }
 
 /* ====================================== large dimensions (64 < d <= 256) ==== */
-/* Dense Gaussian only, d a multiple of 32 (amh_big.hip).  Kernel mirror:
+/* Dense Gaussian only, any 64 < d <= 256 (amh_big.hip).  Kernel mirror:
  *
  * potential  batched over chains on MFMA (v_mfma_f32_32x32x2_f32, a k-ordered
  *            fmaf chain): y_r = fmaf chain over k = 0..d-1 of P_rk D_k with
- *            D = x - m; q_r = D_r y_r; each 32-row tile I is summed as two
+ *            D = x - m; q_r = D_r y_r (q_r = 0 for the rows d .. 32 ceil(d /
+ *            32) - 1 of a ragged last tile); each 32-row tile I is summed as two
  *            sequential halves over the accumulator layout (rows (reg & 3) +
  *            8 (reg >> 2) + 4 h, reg = 0..15, h = 0, 1), t_I = p_I0 + p_I1,
  *            S = sequential sum of t_I over I; U = 0.5 S + c0.
@@ -956,8 +957,9 @@ static float pot_gaussian_big(const orc_cfg* cfg, const float* x) {
     for (int k = 0; k < d; ++k) y = fmaf(P[r * d + k], D[k], y);
     q[r] = D[r] * y;
   }
+  for (int r = d; r < ((d + 31) & ~31); ++r) q[r] = 0.0f; /* a ragged last tile: zero rows */
   float S = 0.0f;
-  for (int I = 0; I < d / 32; ++I) {
+  for (int I = 0; I < (d + 31) / 32; ++I) {
     float ph[2];
     for (int h = 0; h < 2; ++h) {
       float p = 0.0f;
@@ -1611,7 +1613,7 @@ static void asss_chain_step(const orc_cfg* cfg, chain_t* s, uint32_t k0, uint32_
 
 /* n_steps ASSS transitions of chains [0, C) in place (one kernel launch);
  * collect_z [n_steps][C][d] / collect_pe [n_steps][C] nullable. */
-/* ASSS for large dimensions (asss.py:192-269; 64 < d <= 256, d % 32 == 0,
+/* ASSS for large dimensions (asss.py:192-269; 64 < d <= 256,
  * the dense Gaussian; round 5, passes folded in round 6).  Kernel mirror of
  * amh_big.hip asss_big_chain: one wave per chain, lane l owns rows 64 s + l,
  * the factor streamed column by column (the large-d ARWMH path's layout),
@@ -1871,7 +1873,7 @@ static void asss_step_big1(const orc_cfg* cfg, bigchain_t* s, int64_t c, int32_t
 }
 
 static int orc_asss_big(const orc_cfg* cfg) {
-  return cfg->model_id == ORC_GAUSSIAN && cfg->d > ORC_DMAX && cfg->d <= ORC_BIG && cfg->d % 32 == 0;
+  return cfg->model_id == ORC_GAUSSIAN && cfg->d > ORC_DMAX && cfg->d <= ORC_BIG;
 }
 
 void orc_asss_step(const orc_cfg* cfg, int64_t C, int32_t n_steps, int32_t* i_, float* z, float* pe, float* mu,

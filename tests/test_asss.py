@@ -52,7 +52,7 @@ def _step_compare(kind, pre, orc, C=48, d=None):
 @pytest.mark.parametrize("kind,d", [("gaussian", 12), ("gaussian", 64), ("eight_schools", None), ("kidiq", None),
                                     ("diamonds", None), ("mixture", 1), ("mixture", 3),
                                     # large d (asss_step_big1: streamed factor, potential along the circle)
-                                    ("gaussian", 96), ("gaussian", 128)])
+                                    ("gaussian", 96), ("gaussian", 128), ("gaussian", 100), ("gaussian", 97)])
 @pytest.mark.parametrize("pre", [0, 1, 23])
 def test_oracle_step_matches_literal(kind, d, pre, orc):
     _step_compare(kind, pre, orc, C=24 if kind in ("diamonds", "gaussian") else 48, d=d)

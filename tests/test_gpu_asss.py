@@ -52,7 +52,9 @@ def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
                                       ("diamonds", None, 66), ("diamonds_ss", None, 300), ("mixture", 1, 1000),
                                       ("mixture", 3, 200),
                                       # large d (amh_big.hip asss_big_step_kernel, round 5)
-                                      ("gaussian", 96, 130), ("gaussian", 128, 100), ("gaussian", 256, 70)])
+                                      ("gaussian", 96, 130), ("gaussian", 128, 100), ("gaussian", 256, 70),
+                                      # any 64 < d <= 256 (round 6): ragged tile / dword DMA / odd d
+                                      ("gaussian", 72, 90), ("gaussian", 100, 77), ("gaussian", 97, 65)])
 def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
     """ASSS.sample (one launch per step, out of place) vs oracle, 25 steps."""
     k, st, om, ost = _init(kind, C, orc, d=d, num_warmup=8)
@@ -97,7 +99,7 @@ def test_asss_sample_pnx_bitexact(gpu, orc):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("d", [128, 256])
+@pytest.mark.parametrize("d", [128, 256, 100])
 def test_asss_sample_pnx_large_d_bitexact(d, gpu, orc):
     """The large-d frozen kernel (asss_big_pnx_kernel) vs orc_asss_sample_pnx."""
     from kernels_amd import PRNGKey

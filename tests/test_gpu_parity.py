@@ -34,7 +34,8 @@ def test_init_bitexact(kind, gpu, orc):
 
 @pytest.mark.parametrize("kind,d", [("gaussian", 64), ("gaussian", 5), ("gaussian", 16), ("gaussian", 33),
                                     ("eight_schools", None), ("kidiq", None), ("diamonds", None), ("diamonds_ss", None),
-                                    ("gaussian", 96), ("gaussian", 256), ("mixture", 1), ("mixture", 3),
+                                    ("gaussian", 96), ("gaussian", 256), ("gaussian", 72), ("gaussian", 100),
+                                    ("gaussian", 97), ("mixture", 1), ("mixture", 3),
                                     ("mixture", 16)])
 def test_potential_bitexact(kind, d, gpu, orc):
     k, st, om, ost = _init(kind, 8, gpu, orc, d=d)
@@ -112,7 +113,7 @@ def test_split_path_generic_k(gpu, orc):
     np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
 
 
-@pytest.mark.parametrize("d,C,steps", [(128, 77, 12), (256, 33, 6)])
+@pytest.mark.parametrize("d,C,steps", [(128, 77, 12), (256, 33, 6), (72, 70, 8), (100, 65, 8), (97, 41, 8)])
 def test_big_dim_bitexact(d, C, steps, gpu, orc):
     """64 < d <= 256 (amh_big.hip: propose pass, MFMA potential, step pass):
     init, single launches (gamma_1 = 1 keep-L at step 1, the warmup reset at
@@ -148,7 +149,7 @@ def test_sample_pnx_bitexact(gpu, orc):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("d", [96, 128, 256])
+@pytest.mark.parametrize("d", [96, 128, 256, 100, 97])
 def test_sample_pnx_large_d_bitexact(d, gpu, orc):
     """ARWMH.sample_Pnx at 64 < d <= 256 (big_pnx_kernel: the shared factor
     streamed per step, U by P's rows in the MFMA potential's order) against

@@ -368,3 +368,17 @@ def test_rccl_branch_one_rank_bitexact(K):
     print(r.stdout[-2000:], r.stderr[-2000:])
     assert r.returncode == 0
     assert "bit-equal to the fused path" in r.stdout
+
+
+def test_pooled_rejects_unsupported_large_d(gpu):
+    """d > 64 off the 32-multiples binds (regime A, sample_Pnx and ASSS take
+    any d up to 256), but the pooled mode's MFMA tiles need d % 32 == 0: its
+    stats call fails with AMH_EINVAL instead of running the d <= 64 kernels."""
+    from kernels_amd import PooledARWMH, PRNGKey
+    from kernels_amd._lib import AmhError
+    kw, mk, om = make_case("gaussian", 100)
+    k = PooledARWMH(num_chains=64, **kw)
+    z0 = np.random.default_rng(0).uniform(-2, 2, size=(64, 100)).astype(np.float32)
+    st = k.init(PRNGKey(0), 0, torch.as_tensor(z0), (), mk)
+    with pytest.raises(AmhError, match="d % 32 == 0"):
+        k.sample(st)

@@ -90,7 +90,10 @@ def test_nan_potential_rejects():
 # ------------------------------------------------- C oracle vs literal numpy --
 @pytest.mark.parametrize("kind,dim", [("gaussian", 12), ("eight_schools", None), ("kidiq", None),
                                       ("diamonds", None), ("diamonds_ss", None), ("gaussian", 128),
-                                      ("gaussian", 256), ("mixture", 1), ("mixture", 3)])
+                                      ("gaussian", 256), ("mixture", 1), ("mixture", 3),
+                                      # large d off the 32-multiples: a ragged MFMA tile,
+                                      # dword-DMA column blocks, an odd d
+                                      ("gaussian", 72), ("gaussian", 100), ("gaussian", 97)])
 @pytest.mark.parametrize("pre_steps", [0, 1, 37])
 def test_oracle_step_matches_literal(kind, dim, pre_steps, orc):
     """One teacher-forced transition (identical noise) of the C oracle against

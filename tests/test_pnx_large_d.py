@@ -37,7 +37,7 @@ def _split_keys(key, n):
     return np.stack([o[0], o[1]], axis=-1)
 
 
-@pytest.mark.parametrize("d", [96, 128, 256])
+@pytest.mark.parametrize("d", [96, 128, 256, 72, 100, 97])
 def test_one_step_matches_literal(d, orc):
     from kernels_amd import PRNGKey
     g, om, Sigma = _case(d)
