@@ -113,6 +113,8 @@ class PooledARWMH(ARWMH):
             raise ValueError(f"num_warmup ({num_warmup}) must be a multiple of sync_every ({self.sync_every})")
         st = super().init(rng_key, num_warmup, init_params, model_args, model_kwargs)
         d, dev = self._dim, st.z.device
+        if d > 64 and d % 32 != 0:  # the pooled MFMA tiles (amh_pooled_stats returns AMH_EINVAL)
+            raise ValueError(f"the pooled mode takes d <= 64 or a multiple of 32 up to 256, not d = {d}")
         f = dict(dtype=torch.float32, device=dev)
         eye = torch.eye(d, dtype=torch.float64, device=dev)
         from .arwmh import pack_scale

@@ -372,13 +372,28 @@ def test_rccl_branch_one_rank_bitexact(K):
 
 def test_pooled_rejects_unsupported_large_d(gpu):
     """d > 64 off the 32-multiples binds (regime A, sample_Pnx and ASSS take
-    any d up to 256), but the pooled mode's MFMA tiles need d % 32 == 0: its
-    stats call fails with AMH_EINVAL instead of running the d <= 64 kernels."""
-    from kernels_amd import PooledARWMH, PRNGKey
+    any d up to 256), but the pooled mode's MFMA tiles need d % 32 == 0:
+    PooledARWMH.init raises ValueError, and the C entry itself returns
+    AMH_EINVAL instead of running the d <= 64 kernels."""
+    import ctypes
+    from kernels_amd import ARWMH, PooledARWMH, PRNGKey, _lib
     from kernels_amd._lib import AmhError
     kw, mk, om = make_case("gaussian", 100)
-    k = PooledARWMH(num_chains=64, **kw)
-    z0 = np.random.default_rng(0).uniform(-2, 2, size=(64, 100)).astype(np.float32)
-    st = k.init(PRNGKey(0), 0, torch.as_tensor(z0), (), mk)
+    z0 = torch.as_tensor(np.random.default_rng(0).uniform(-2, 2, size=(64, 100)).astype(np.float32))
+    with pytest.raises(ValueError, match="pooled mode"):
+        PooledARWMH(num_chains=64, **kw).init(PRNGKey(0), 0, z0, (), mk)
+    k = ARWMH(num_chains=64, **kw)  # a handle bound to d = 100, driven through the pooled C entry
+    st = k.init(PRNGKey(0), 0, z0, (), mk)
+    dev = st.z.device
+    cov = torch.zeros(100 * 101 // 2, dtype=torch.float64, device=dev)
+    one = torch.zeros(1, dtype=torch.float32, device=dev)
+    ps = _lib.AmhPooledState(torch.zeros(1, dtype=torch.int32, device=dev).data_ptr(), st.z.data_ptr(),
+                             st.potential_energy.data_ptr(), st.rng_key.data_ptr(), one.data_ptr(),
+                             st.adapt_state.loc.data_ptr(), st.adapt_state.scale.data_ptr(), one.data_ptr(),
+                             one.data_ptr(), cov.data_ptr())
+    zo, po = torch.empty_like(st.z), torch.empty_like(st.potential_energy)
+    sums = torch.zeros(100 + 5050 + 2, dtype=torch.float64, device=dev)
+    rc = _lib.lib().amh_pooled_stats(k._handle.h, 64, ctypes.byref(ps), _lib.ptr(zo), _lib.ptr(po), _lib.ptr(sums),
+                                     _lib.stream_ptr(dev.index))
     with pytest.raises(AmhError, match="d % 32 == 0"):
-        k.sample(st)
+        _lib.check(rc, k._handle.h)
