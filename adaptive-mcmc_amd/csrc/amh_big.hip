@@ -33,7 +33,7 @@ namespace amh {
 
 namespace {
 
-constexpr int kNS = 4;  // row slots per lane: d <= 64 * kNS
+constexpr int kNSMAX = 4;  // row slots per lane: d <= 64 * NS, NS = 2 (d <= 128) or 4
 constexpr int kAsssBigMaxIter = 50;  // asss.py:59 max_iterations
 #ifndef AMH_ABL_NOPASSD
 #define AMH_ABL_NOPASSD 0
@@ -51,9 +51,17 @@ __device__ __forceinline__ float big_gamma(const BigParams& p, int32_t n) {
 }
 
 // sum over rows: 64-lane butterfly per slot, then (s0 + s1) + (s2 + s3)
-__device__ __forceinline__ float big_sum(const float (&v)[kNS]) {
-  float s[kNS];
-  static_for<kNS>([&](auto K) { s[K] = Grp<64>::sum(v[K]); });
+// (NS = 2: s2 = s3 = +0, added as such -- the bits of the four-slot form)
+template <int NS>
+__device__ __forceinline__ float big_sum(const float (&v)[NS]) {
+  float s[kNSMAX];
+  static_for<kNSMAX>([&](auto K) {
+    if constexpr (K < NS) {
+      s[K] = Grp<64>::sum(v[K]);
+    } else {
+      s[K] = 0.0f;
+    }
+  });
   return (s[0] + s[1]) + (s[2] + s[3]);
 }
 
@@ -93,12 +101,12 @@ __device__ __forceinline__ void issue_block(const float* Lc, int d, int64_t P, i
 // f(KB, j, v) for every column j in order, v[K] = L_rj for rows r = 64 K + l
 // (only rows j < r < d are meaningful; the diagonal L_jj is v[j / 64] of
 // lane j % 64).  KB = j / 64 is a compile-time slot index.
-template <bool RAG, class F>
+template <bool RAG, int NS, class F>
 __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, float* wb0, float* wb1, int lane,
                                             F&& f) {
   const int nb = (d + kColBlk - 1) / kColBlk;
   issue_block<RAG>(Lc, d, P, 0, wb0, lane);
-  static_for<kNS>([&](auto KB) {
+  static_for<NS>([&](auto KB) {
     constexpr int kb = KB;
     if (64 * kb < d) {
       for (int bb = 0; bb < 64 / kColBlk; ++bb) {
@@ -112,10 +120,10 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         // element (r, j) sits at cur[col_off(d, j) - ob + r - j]; column q + 1's
         // reads are issued before f runs on column q (one LDS round trip off
         // each column but the block's first)
-        auto rd = [&](int q, float (&v)[kNS]) {
+        auto rd = [&](int q, float (&v)[NS]) {
           const int j = kColBlk * b + q;
           const uint32_t a0 = lds_addr(cur) + 4u * (uint32_t)(col_off(d, j) - ob - j + lane);
-          static_for<kNS>([&](auto K) {
+          static_for<NS>([&](auto K) {
             if constexpr (K >= kb) {
               v[K] = lds_ld1<0>(a0 + 256u * K);
             } else {
@@ -125,16 +133,16 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         };
         // (the wait sits at the end of the iteration, so no loop-carried
         // register is copied while its read is in flight)
-        float vn[kNS];
+        float vn[NS];
         rd(0, vn);
-        lds_wait(vn[0], vn[1], vn[2], vn[3]);
+        lds_wait_n(vn);
         // RAG (d % 8 != 0): a run-time column count for the ragged last
         // block; the aligned instantiation keeps the compile-time trip count
         // (a run-time bound in it cost 12-17 % at d = 256)
         const int qn = RAG ? ((d - kColBlk * b) < kColBlk ? (d - kColBlk * b) : kColBlk) : kColBlk;
         for (int q = 0; q < qn; ++q) {
-          float v[kNS];
-          static_for<kNS>([&](auto K) { v[K] = vn[K]; });
+          float v[NS];
+          static_for<NS>([&](auto K) { v[K] = vn[K]; });
 #if AMH_BIG_NOPIPE
           f(KB, kColBlk * b + q, v);
           if (q + 1 < qn) rd(q + 1, vn);
@@ -142,7 +150,7 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
           if (q + 1 < qn) rd(q + 1, vn);
           f(KB, kColBlk * b + q, v);
 #endif
-          lds_wait(vn[0], vn[1], vn[2], vn[3]);
+          lds_wait_n(vn);
         }
       }
     }
@@ -154,6 +162,7 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
 // --------------------------------------------------------------- init ----
 // arwmh.py:84-138 (init_to_uniform), one wave per chain; pe0 is filled by
 // the MFMA potential afterwards.
+template <int NS>
 __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
   const int d = p.d;
   const int lane = lane_id();
@@ -162,7 +171,7 @@ __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
   for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < p.C; c += nw) {
     const uint64_t gc = (uint64_t)(p.chain_offset + c);
     const amh_u32x4 kk = amh_philox4x32_10((uint32_t)gc, (uint32_t)(gc >> 32), 0u, AMH_TAG_CHAINKEY, p.key0, p.key1);
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) {
         float z0;
@@ -179,7 +188,7 @@ __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
     });
     float* Lc = p.out.scale + c * P;
     for (int j = 0; j < d; ++j) {
-      static_for<kNS>([&](auto K) {
+      static_for<NS>([&](auto K) {
         const int r = 64 * K + lane;
         if (r >= j && r < d) Lc[col_off(d, j) + (r - j)] = (r == j) ? 1.0f : 0.0f;
       });
@@ -197,7 +206,7 @@ __global__ __launch_bounds__(256) void big_init_kernel(InitParams p) {
 }
 
 // ------------------------------------------------------------- propose ----
-template <bool RAG>
+template <bool RAG, int NS>
 __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -212,10 +221,10 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
     const int32_t it = p.in.i[c];
     const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
     const float el = amh_expf(p.in.log_step_size[c]);
-    float inv[kNS], xi[kNS], eta[kNS], zz[kNS], mu[kNS], acc[kNS], sa[kNS], sr[kNS], zp[kNS], wa[kNS], wr[kNS];
-    float pdl[kNS];
-    step_noise_rows<kNS>(lane, d, (uint32_t)it, k0, k1, xi);  // bit spec: amh_step_word
-    static_for<kNS>([&](auto K) {
+    float inv[NS], xi[NS], eta[NS], zz[NS], mu[NS], acc[NS], sa[NS], sr[NS], zp[NS], wa[NS], wr[NS];
+    float pdl[NS];
+    step_noise_rows<NS>(lane, d, (uint32_t)it, k0, k1, xi);  // bit spec: amh_step_word
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       const float dl = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
@@ -226,7 +235,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
       mu[K] = act ? p.in.loc[c * d + r] : 0.0f;
       acc[K] = sa[K] = sr[K] = zp[K] = wa[K] = wr[K] = 0.0f;
     });
-    for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+    for_columns<RAG, NS>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[NS]) {
       constexpr int kb = KB;
       const int jl = j - 64 * kb;
       const float etaj = rdl(eta[kb], jl);
@@ -240,7 +249,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
       }
       const float waj = rdl(wa[kb], jl);
       const float wrj = rdl(wr[kb], jl);
-      static_for<kNS>([&](auto K) {
+      static_for<NS>([&](auto K) {
         if constexpr (K >= kb) {
           const int r = 64 * K + lane;
           if (r > j && r < d) {
@@ -252,7 +261,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
         }
       });
     });
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) {
         p.xprop[c * d + r] = zp[K];
@@ -270,7 +279,7 @@ __global__ __launch_bounds__(256) void big_propose_kernel(BigParams p) {
 // big_propose_kernel on the stored values), so a multi-step launch reads the
 // factor once per transition.  The wave's own xprop / wa / wr rows were read
 // at the top of its chain, so the next ones overwrite them in place.
-template <bool NEXT, bool RAG>
+template <bool NEXT, bool RAG, int NS>
 __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -302,8 +311,8 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
     const float e1 = amh_expf(lamn);
     const float el = amh_expf(lam);
     const float sq = sqrtf(1.0f - gamma);
-    float dl[kNS], inv[kNS], zn[kNS], delta[kNS], mun[kNS], ws[kNS], Dg[kNS], one[kNS], gw2[kNS], t[kNS];
-    static_for<kNS>([&](auto K) {
+    float dl[NS], inv[NS], zn[NS], delta[NS], mun[NS], ws[NS], Dg[NS], one[NS], gw2[NS], t[NS];
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       dl[K] = act ? p.dg[c * d + r] : 0.0f;  // the diagonal, coalesced (propose / previous step pass)
@@ -323,10 +332,10 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       t[K] = act ? gw2[K] / Dg[K] : 0.0f;
     });
     // b_j: 64-lane exclusive scan per slot plus the carry of the slots before
-    float cc[kNS], qq[kNS];
+    float cc[NS], qq[NS];
     bool bad = false;
     float carry = 0.0f;
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       const float e = Grp<64>::excl_scan(t[K], lane);
@@ -342,13 +351,13 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       bad = bad || (act && amh_isnan(dnew));
     });
     const bool revert = __ballot(bad) != 0ull;
-    float sacc[kNS];
-    static_for<kNS>([&](auto K) { sacc[K] = 0.0f; });
+    float sacc[NS];
+    static_for<NS>([&](auto K) { sacc[K] = 0.0f; });
     // next transition's propose state (big_propose_kernel on the output state)
-    float ninv[kNS], nxi[kNS], neta[kNS], nacc[kNS], nsa[kNS], nsr[kNS], nzp[kNS], nwa[kNS], nwr[kNS], ndg[kNS];
+    float ninv[NS], nxi[NS], neta[NS], nacc[NS], nsa[NS], nsr[NS], nzp[NS], nwa[NS], nwr[NS], ndg[NS];
     if constexpr (NEXT) {
-      step_noise_rows<kNS>(lane, d, (uint32_t)itr, k0, k1, nxi);
-      static_for<kNS>([&](auto K) {
+      step_noise_rows<NS>(lane, d, (uint32_t)itr, k0, k1, nxi);
+      static_for<NS>([&](auto K) {
         const int r = 64 * K + lane;
         const bool act = r < d;
         const float ndl = act ? (revert ? dl[K] : 1.0f * qq[K]) : 0.0f;
@@ -359,7 +368,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       });
     }
     // column j of L' (rows > j in nv) into the next proposal and both solves
-    auto next_col = [&](auto KB, int j, const float (&nv)[kNS]) {
+    auto next_col = [&](auto KB, int j, const float (&nv)[NS]) {
       if constexpr (NEXT) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
@@ -373,7 +382,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
         }
         const float waj = rdl(nwa[kb], jl);
         const float wrj = rdl(nwr[kb], jl);
-        static_for<kNS>([&](auto K) {
+        static_for<NS>([&](auto K) {
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r > j && r < d) {
@@ -387,13 +396,13 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       }
     };
     if (!revert) {
-      float ac[kNS], bc[kNS], sv[kNS];
-      static_for<kNS>([&](auto K) {
+      float ac[NS], bc[NS], sv[NS];
+      static_for<NS>([&](auto K) {
         ac[K] = (qq[K] * e1) - (dl[K] * el);
         bc[K] = (cc[K] * qq[K]) * e1;
         sv[K] = 0.0f;
       });
-      for_columns<RAG>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+      for_columns<RAG, NS>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[NS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
@@ -404,8 +413,8 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
           sacc[kb] = fmaf(tt, tt, sacc[kb]);
           ocol[j] = 1.0f * qj;
         }
-        float nv[kNS];
-        static_for<kNS>([&](auto K) {
+        float nv[NS];
+        static_for<NS>([&](auto K) {
           nv[K] = 0.0f;
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
@@ -425,9 +434,9 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       });
     } else {
       // factor kept (arwmh.py:191): copied verbatim; as_change = ||L (e1 - e0)||_F
-      float ac[kNS];
-      static_for<kNS>([&](auto K) { ac[K] = (dl[K] * e1) - (dl[K] * el); });
-      for_columns<RAG>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[kNS]) {
+      float ac[NS];
+      static_for<NS>([&](auto K) { ac[K] = (dl[K] * e1) - (dl[K] * el); });
+      for_columns<RAG, NS>(Lin, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&v)[NS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float acj = rdl(ac[kb], jl), invj = rdl(inv[kb], jl);
@@ -437,7 +446,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
           sacc[kb] = fmaf(t0, t0, sacc[kb]);
           ocol[j] = dl[kb];
         }
-        static_for<kNS>([&](auto K) {
+        static_for<NS>([&](auto K) {
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r > j && r < d) {
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(256) void big_step_kernel(BigParams p) {
       });
     }
     const float asc = sqrtf(big_sum(sacc));
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) {
         p.out.z[c * d + r] = zn[K];
@@ -615,9 +624,9 @@ __global__ __launch_bounds__(256) void gauss_pot_mfma_kernel(PotParams p) {
 // ADAPT = false is the frozen kernel of sample_Pnx (shared loc / factor).
 namespace {
 
-template <bool ADAPT, bool RAG>
-__device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, const float (&dl)[kNS],
-                                               const float (&inv)[kNS], float (&x)[kNS], float (&mu)[kNS],
+template <bool ADAPT, bool RAG, int NS>
+__device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, const float (&dl)[NS],
+                                               const float (&inv)[NS], float (&x)[NS], float (&mu)[NS],
                                                float& pe, float& asc, int32_t it, uint32_t k0, uint32_t k1, int d,
                                                int64_t P, float eps, int32_t W, float gamma_in, const ModelArgs& model,
                                                float* wb0, float* wb1, int lane) {
@@ -628,8 +637,8 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   const float epsd = eps * sd;
   const float fd = (float)d;
   // ---- draws (asss.py:207, 219, 225, 60): the d <= 64 kernel's stream
-  float v[kNS];
-  static_for<kNS>([&](auto K) {
+  float v[NS];
+  static_for<NS>([&](auto K) {
     const int r = 64 * K + lane;
     v[K] = (r < d) ? amh_normal_from_bits(amh_philox4x32_10((uint32_t)r, (uint32_t)it, 0u, AMH_TAG_ASSS, k0, k1).v[0])
                    : 0.0f;
@@ -639,8 +648,8 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   const float ut = amh_unif01_from_bits(o0.v[2]);
   const float th0 = 6.28318548f * amh_unif01_from_bits(o0.v[3]);
   // ---- pass A: y = S^-1 (x - mu), av = U (e v), wy = U^-1 y, wv = U^-1 v
-  float e[kNS], invD[kNS], b[kNS], y[kNS], tt[kNS], hv[kNS], av[kNS], ty[kNS], tv[kNS], wy[kNS], wv[kNS];
-  static_for<kNS>([&](auto K) {
+  float e[NS], invD[NS], b[NS], y[NS], tt[NS], hv[NS], av[NS], ty[NS], tv[NS], wy[NS], wv[NS];
+  static_for<NS>([&](auto K) {
     const bool act = 64 * K + lane < d;
     e[K] = dl[K] * sd;
     invD[K] = 1.0f / ((dl[K] + eps) * sd);
@@ -649,7 +658,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     y[K] = av[K] = ty[K] = tv[K] = wy[K] = wv[K] = 0.0f;
   });
 #if !AMH_ABL_NOPASSA
-  for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+  for_columns<RAG, NS>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[NS]) {
     constexpr int kb = KB;
     const int jl = j - 64 * kb;
     const float yl = rdl(b[kb] * invD[kb], jl);
@@ -667,7 +676,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       wy[kb] = wyj;
       wv[kb] = wvj;
     }
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       if constexpr (K >= kb) {
         const int r = 64 * K + lane;
         if (r > j && r < d) {
@@ -683,27 +692,27 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     });
   });
 #endif
-  float svr[kNS];  // S v for the raw draw
-  static_for<kNS>([&](auto K) { svr[K] = av[K] + epsd * v[K]; });
+  float svr[NS];  // S v for the raw draw
+  static_for<NS>([&](auto K) { svr[K] = av[K] + epsd * v[K]; });
   // ---- stereographic projection, tangent v (asss.py:40-45, 219-222)
-  static_for<kNS>([&](auto K) { tt[K] = y[K] * y[K]; });
+  static_for<NS>([&](auto K) { tt[K] = y[K] * y[K]; });
   const float ns = big_sum(tt);
   const float den = ns + 1.0f;
-  float zr[kNS];
-  static_for<kNS>([&](auto K) { zr[K] = (2.0f * y[K]) / den; });
+  float zr[NS];
+  static_for<NS>([&](auto K) { zr[K] = (2.0f * y[K]) / den; });
   const float zd = (ns - 1.0f) / den;
-  static_for<kNS>([&](auto K) { tt[K] = v[K] * zr[K]; });
+  static_for<NS>([&](auto K) { tt[K] = v[K] * zr[K]; });
   const float dot = big_sum(tt) + (vd * zd);
-  static_for<kNS>([&](auto K) { v[K] = (64 * K + lane < d) ? fmaf(-dot, zr[K], v[K]) : 0.0f; });
+  static_for<NS>([&](auto K) { v[K] = (64 * K + lane < d) ? fmaf(-dot, zr[K], v[K]) : 0.0f; });
   vd = fmaf(-dot, zd, vd);
-  static_for<kNS>([&](auto K) { tt[K] = v[K] * v[K]; });
+  static_for<NS>([&](auto K) { tt[K] = v[K] * v[K]; });
   const float nv = sqrtf(big_sum(tt) + (vd * vd));
   const bool degen = !(nv > 0.0f);  // the d <= 64 kernel's rule (amh_asss.h)
-  static_for<kNS>([&](auto K) { v[K] = degen ? 0.0f : v[K] / nv; });
+  static_for<NS>([&](auto K) { v[K] = degen ? 0.0f : v[K] / nv; });
   vd = degen ? 0.0f : vd / nv;
   // ---- S z = 2 (x - mu) / den, S v = (S v_raw - dot S z) / |v|; U^-1 z, U^-1 v
-  float Sz[kNS], Sv[kNS], Wz[kNS], Wv[kNS], gm[kNS], Pa[kNS], Pb[kNS], Pg[kNS];
-  static_for<kNS>([&](auto K) {
+  float Sz[NS], Sv[NS], Wz[NS], Wv[NS], gm[NS], Pa[NS], Pb[NS], Pg[NS];
+  static_for<NS>([&](auto K) {
     const int r = 64 * K + lane;
     const bool act = r < d;
     Sz[K] = act ? (2.0f * (x[K] - mu[K])) / den : 0.0f;
@@ -717,21 +726,21 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   });
   // ---- P a, P b, P g: row k of P (= column k) coalesced, k in order
 #if !AMH_ABL_NOPMV  // (timing ablations only: AMH_ABL_*)
-  static_for<kNS>([&](auto KB) {
+  static_for<NS>([&](auto KB) {
     constexpr int kb = KB;
     if (64 * kb < d) {
       const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;
       for (int k2 = 0; k2 < kmax; k2 += 8) {
-        float pr[8][kNS];  // rows k >= d read as zeros (their terms leave the chains unchanged)
+        float pr[8][NS];  // rows k >= d read as zeros (their terms leave the chains unchanged)
         static_for<8>([&](auto T) {
           const bool kin = !RAG || k2 + T < kmax;  // d % 8 == 0: kmax is a multiple of 8
           const float* row = Pm + (int64_t)(kin ? 64 * kb + k2 + T : 0) * d;
-          static_for<kNS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+          static_for<NS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
         });
         static_for<8>([&](auto T) {
           const int kl = k2 + T;
           const float sa = rdl(Sz[kb], kl), sb = rdl(Sv[kb], kl), sg = rdl(gm[kb], kl);
-          static_for<kNS>([&](auto K) {
+          static_for<NS>([&](auto K) {
             Pa[K] = fmaf(pr[T][K], sa, Pa[K]);
             Pb[K] = fmaf(pr[T][K], sb, Pb[K]);
             Pg[K] = fmaf(pr[T][K], sg, Pg[K]);
@@ -742,10 +751,10 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   });
 #endif
   // the point at angle (cs, sn) of the slice circle: x and U
-  auto eval = [&](float cs, float sn, float (&xo)[kNS], float& om) -> float {
+  auto eval = [&](float cs, float sn, float (&xo)[NS], float& om) -> float {
     om = 1.0f - ((zd * cs) + (vd * sn));
-    float t4[kNS];
-    static_for<kNS>([&](auto K) {
+    float t4[NS];
+    static_for<NS>([&](auto K) {
       const bool act = 64 * K + lane < d;
       const float num = (Sz[K] * cs) + (Sv[K] * sn);
       const float Dr = (num / om) + gm[K];
@@ -756,7 +765,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     return (0.5f * big_sum(t4)) + c0;
   };
   // ---- slice level and shrinkage (asss.py:216-239, 59-96)
-  float x0[kNS], xt[kNS], om0;
+  float x0[NS], xt[NS], om0;
   const float U0 = eval(1.0f, 0.0f, x0, om0);
   const float tpe = (U0 + fd * amh_logf(om0)) - amh_logf(ut);
   float th = th0, thmin = th0 - 6.28318548f, thmax = th0;
@@ -796,12 +805,12 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     snt = 0.0f;
     omt = om0;
   }
-  float xn[kNS];
-  static_for<kNS>([&](auto K) { xn[K] = capped ? x0[K] : xt[K]; });
+  float xn[NS];
+  static_for<NS>([&](auto K) { xn[K] = capped ? x0[K] : xt[K]; });
   float pen = capped ? U0 : ux;
   if (amh_isnan(pen)) pen = INFINITY;
   if constexpr (!ADAPT) {
-    static_for<kNS>([&](auto K) { x[K] = xn[K]; });
+    static_for<NS>([&](auto K) { x[K] = xn[K]; });
     pe = pen;
     (void)Lout;
     (void)W;
@@ -811,9 +820,9 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
   } else {
     // ---- adaptation (asss.py:246-267): mean, rank-one update, as_change
     const float gamma = gamma_in;
-    float delta[kNS], mun[kNS], Dg[kNS], one[kNS], ws[kNS], gw2[kNS];
+    float delta[NS], mun[NS], Dg[NS], one[NS], ws[NS], gw2[NS];
     const float sq = sqrtf(1.0f - gamma);
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const bool act = 64 * K + lane < d;
       delta[K] = act ? xn[K] - mu[K] : 0.0f;
       mun[K] = act ? mu[K] + gamma * delta[K] : 0.0f;
@@ -828,11 +837,11 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       ws[K] = act ? ((dl[K] * q) + (eps * wq)) * sd : 0.0f;
     });
     const float locd = sqrtf(big_sum(tt));
-    float cc[kNS], qq[kNS];
+    float cc[NS], qq[NS];
     bool bad = false;
     {
       float carry = 0.0f;
-      static_for<kNS>([&](auto K) {
+      static_for<NS>([&](auto K) {
         const bool act = 64 * K + lane < d;
         gw2[K] = act ? gamma * (ws[K] * ws[K]) : 0.0f;
         const float t = act ? gw2[K] / Dg[K] : 0.0f;
@@ -854,13 +863,13 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
     if (!revert) {
       // pass D: the update, L' streamed out (in place allowed: block b + 1 is
       // in flight before block b's columns are written)
-      float ac[kNS], bc[kNS], sv[kNS], sacc[kNS];
-      static_for<kNS>([&](auto K) {
+      float ac[NS], bc[NS], sv[NS], sacc[NS];
+      static_for<NS>([&](auto K) {
         ac[K] = qq[K] - dl[K];
         bc[K] = cc[K] * qq[K];
         sv[K] = sacc[K] = 0.0f;
       });
-      for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      for_columns<RAG, NS>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[NS]) {
         constexpr int kb = KB;
         const int jl = j - 64 * kb;
         const float wsj = rdl(ws[kb], jl), cj = rdl(cc[kb], jl), acj = rdl(ac[kb], jl);
@@ -871,7 +880,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
           sacc[kb] = fmaf(t0, t0, sacc[kb]);
           ocol[j] = 1.0f * qj;
         }
-        static_for<kNS>([&](auto K) {
+        static_for<NS>([&](auto K) {
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r > j && r < d) {
@@ -888,10 +897,10 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       });
       sdiff = sqrtf(big_sum(sacc));
     } else if (Lout != Lc && !AMH_ABL_NOPASSD) {  // factor kept (asss.py:255): copied verbatim
-      for_columns<RAG>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      for_columns<RAG, NS>(Lc, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[NS]) {
         constexpr int kb = KB;
         float* ocol = Lout + col_off(d, j) - j;
-        static_for<kNS>([&](auto K) {
+        static_for<NS>([&](auto K) {
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r >= j && r < d) ocol[r] = vv[K];
@@ -900,7 +909,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
       });
     }
     asc = locd + sdiff;
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       x[K] = xn[K];
       mu[K] = mun[K];
     });
@@ -911,7 +920,7 @@ __device__ __forceinline__ void asss_big_chain(const float* Lc, float* Lout, con
 }  // namespace
 
 // ASSS.sample: one transition of every chain per launch (host loops n_steps)
-template <bool RAG>
+template <bool RAG, int NS>
 __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -927,8 +936,8 @@ __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
     float* Lo = p.out.scale + c * P;
     const int32_t it = p.in.i[c];
     const uint32_t k0 = p.in.rng_key[2 * c], k1 = p.in.rng_key[2 * c + 1];
-    float dl[kNS], inv[kNS], x[kNS], mu[kNS];
-    static_for<kNS>([&](auto K) {
+    float dl[NS], inv[NS], x[NS], mu[NS];
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       dl[K] = act ? Lc[col_off(d, act ? r : 0)] : 0.0f;
@@ -941,9 +950,9 @@ __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
     const float gamma = (n < p.gamma_tab_n) ? ((const cf*)p.gamma_tab)[n] : amh_lr_gamma(n, p.a);
     float pe = p.in.potential_energy[c];
     float asc = 0.0f;
-    asss_big_chain<true, RAG>(Lc, Lo, dl, inv, x, mu, pe, asc, it, k0, k1, d, P, p.eps, p.W, gamma, p.model, wb0, wb1,
+    asss_big_chain<true, RAG, NS>(Lc, Lo, dl, inv, x, mu, pe, asc, it, k0, k1, d, P, p.eps, p.W, gamma, p.model, wb0, wb1,
                          lane);
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) {
         p.out.z[c * d + r] = x[K];
@@ -965,7 +974,7 @@ __global__ __launch_bounds__(256) void asss_big_step_kernel(StepParams p) {
 // ASSS.sample_Pnx: chain c = (point, sample) from x[point] with key split(c),
 // n frozen transitions with the shared (loc, factor), the transition's
 // stream position the step index
-template <bool RAG>
+template <bool RAG, int NS>
 __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -976,8 +985,8 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
   const int64_t P = (int64_t)d * (d + 1) / 2;
   const int64_t nw = (int64_t)gridDim.x * 4;
   const int64_t C = p.n_points * p.n_samples;
-  float dl[kNS], inv[kNS];
-  static_for<kNS>([&](auto K) {
+  float dl[NS], inv[NS];
+  static_for<NS>([&](auto K) {
     const int r = 64 * K + lane;
     const bool act = r < d;
     dl[K] = act ? p.scale[col_off(d, act ? r : 0)] : 0.0f;
@@ -986,8 +995,8 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
   for (int64_t c = (int64_t)blockIdx.x * 4 + threadIdx.x / 64; c < C; c += nw) {
     const int64_t pt = c / p.n_samples;
     const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, p.key0, p.key1);
-    float x[kNS], mu[kNS];
-    static_for<kNS>([&](auto K) {
+    float x[NS], mu[NS];
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       x[K] = act ? p.x[pt * d + r] : 0.0f;
@@ -995,9 +1004,9 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
     });
     float pe = 0.0f, asc = 0.0f;
     for (int32_t t = 0; t < p.n; ++t)
-      asss_big_chain<false, RAG>(p.scale, nullptr, dl, inv, x, mu, pe, asc, t, kk.v[0], kk.v[1], d, P, p.eps, 0, 0.0f,
+      asss_big_chain<false, RAG, NS>(p.scale, nullptr, dl, inv, x, mu, pe, asc, t, kk.v[0], kk.v[1], d, P, p.eps, 0, 0.0f,
                             p.model, wb0, wb1, lane);
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) p.out[c * d + r] = x[K];
     });
@@ -1011,7 +1020,7 @@ __global__ __launch_bounds__(256) void asss_big_pnx_kernel(AsssPnxParams p) {
 // L_rj xi_j over j <= r, rows r = 64 s + l); U(z') takes P's rows in k order
 // (an fmaf chain per row, the MFMA potential's bits) and sums D_r Y_r in the
 // MFMA kernel's tile order (pot_gaussian_big).
-template <bool RAG>
+template <bool RAG, int NS>
 __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
   extern __shared__ float lds_big[];
   const int d = p.d;
@@ -1027,38 +1036,38 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
   const float c0 = p.model.data[d + d * d];
   const float el = amh_expf(p.log_step_size);
   // U(zz) = 0.5 sum_r D_r Y_r + c0, Y = P D, D = zz - m
-  auto potential = [&](const float (&zz)[kNS]) -> float {
-    float D[kNS], Y[kNS];
-    static_for<kNS>([&](auto K) {
+  auto potential = [&](const float (&zz)[NS]) -> float {
+    float D[NS], Y[NS];
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       const bool act = r < d;
       D[K] = act ? zz[K] - m[act ? r : 0] : 0.0f;
       Y[K] = 0.0f;
     });
-    static_for<kNS>([&](auto KB) {
+    static_for<NS>([&](auto KB) {
       constexpr int kb = KB;
       if (64 * kb < d) {
         const int kmax = (d - 64 * kb) < 64 ? (d - 64 * kb) : 64;
         for (int k2 = 0; k2 < kmax; k2 += 8) {
-          float pr[8][kNS];  // rows k >= d read as zeros
+          float pr[8][NS];  // rows k >= d read as zeros
           static_for<8>([&](auto T) {
             const bool kin = !RAG || k2 + T < kmax;  // d % 8 == 0: kmax is a multiple of 8
             const float* row = Pm + (int64_t)(kin ? 64 * kb + k2 + T : 0) * d;  // row k = column k (P symmetric)
-            static_for<kNS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
+            static_for<NS>([&](auto K) { pr[T][K] = (kin && 64 * K + lane < d) ? row[64 * K + lane] : 0.0f; });
           });
           static_for<8>([&](auto T) {
             const float dk = rdl(D[kb], k2 + T);
-            static_for<kNS>([&](auto K) { Y[K] = fmaf(pr[T][K], dk, Y[K]); });
+            static_for<NS>([&](auto K) { Y[K] = fmaf(pr[T][K], dk, Y[K]); });
           });
         }
       }
     });
-    float q[kNS];
-    static_for<kNS>([&](auto K) { q[K] = (64 * K + lane < d) ? D[K] * Y[K] : 0.0f; });
+    float q[NS];
+    static_for<NS>([&](auto K) { q[K] = (64 * K + lane < d) ? D[K] * Y[K] : 0.0f; });
     // tile order: 32-row tiles in order, each (ph_0 + ph_1), ph_h the
     // sequential sum of rows 32 I + (g & 3) + 8 (g >> 2) + 4 h, g = 0..15
     float S = 0.0f;
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       static_for<2>([&](auto I2) {
         if (64 * K + 32 * I2 < d) {
           float ph[2];
@@ -1080,28 +1089,28 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
     const int64_t pt = c / p.n_samples;
     const amh_u32x4 kk = amh_philox4x32_10((uint32_t)c, (uint32_t)((uint64_t)c >> 32), 0u, AMH_TAG_SPLIT, p.key0, p.key1);
     const uint32_t k0 = kk.v[0], k1 = kk.v[1];
-    float z[kNS];
-    static_for<kNS>([&](auto K) {
+    float z[NS];
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       z[K] = (r < d) ? p.x[pt * d + r] : 0.0f;
     });
     float pe = potential(z);
     for (int32_t t = 0; t < p.n; ++t) {
-      float xi[kNS], acc[kNS], zp[kNS];
-      step_noise_rows<kNS>(lane, d, (uint32_t)t, k0, k1, xi);  // bit spec: amh_step_word
+      float xi[NS], acc[NS], zp[NS];
+      step_noise_rows<NS>(lane, d, (uint32_t)t, k0, k1, xi);  // bit spec: amh_step_word
       const float u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)t, k0, k1));  // W_d
-      static_for<kNS>([&](auto K) { acc[K] = 0.0f; });
-      for_columns<RAG>(p.scale, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[kNS]) {
+      static_for<NS>([&](auto K) { acc[K] = 0.0f; });
+      for_columns<RAG, NS>(p.scale, d, P, wb0, wb1, lane, [&](auto KB, int j, const float (&vv)[NS]) {
         constexpr int kb = KB;
         const float xj = rdl(xi[kb], j - 64 * kb);
-        static_for<kNS>([&](auto K) {
+        static_for<NS>([&](auto K) {
           if constexpr (K >= kb) {
             const int r = 64 * K + lane;
             if (r >= j && r < d) acc[K] = fmaf(vv[K], xj, acc[K]);
           }
         });
       });
-      static_for<kNS>([&](auto K) {
+      static_for<NS>([&](auto K) {
         const bool act = 64 * K + lane < d;
         zp[K] = act ? z[K] + fmaf(el, acc[K], p.eps * xi[K]) : 0.0f;
       });
@@ -1110,11 +1119,11 @@ __global__ __launch_bounds__(256) void big_pnx_kernel(PnxParams p) {
       const float ex = amh_expf(pe - pep);
       const float alpha = (ex > 1.0f) ? 1.0f : ex;
       if (u < alpha) {  // wave-uniform: one chain per wave
-        static_for<kNS>([&](auto K) { z[K] = zp[K]; });
+        static_for<NS>([&](auto K) { z[K] = zp[K]; });
         pe = pep;
       }
     }
-    static_for<kNS>([&](auto K) {
+    static_for<NS>([&](auto K) {
       const int r = 64 * K + lane;
       if (r < d) p.out[c * d + r] = z[K];
     });
@@ -1136,37 +1145,45 @@ static int wave_grid(int64_t n) {
 }
 
 hipError_t run_big_init(const InitParams& p, hipStream_t s) {
-  hipLaunchKernelGGL(big_init_kernel, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
+  auto k = (p.d <= 128) ? big_init_kernel<2> : big_init_kernel<4>;
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 static size_t stream_lds(int d) { return (size_t)4 * 2 * kColBlk * d * sizeof(float); }
 hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
-  if (p.d % kColBlk) {
-    hipLaunchKernelGGL(big_propose_kernel<true>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
-  } else {
-    hipLaunchKernelGGL(big_propose_kernel<false>, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
-  }
+  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
+  auto k = rag ? (two ? big_propose_kernel<true, 2> : big_propose_kernel<true, 4>)
+               : (two ? big_propose_kernel<false, 2> : big_propose_kernel<false, 4>);
+  hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
-  const bool rag = p.d % kColBlk != 0;
-  auto k = next ? (rag ? big_step_kernel<true, true> : big_step_kernel<true, false>)
-                : (rag ? big_step_kernel<false, true> : big_step_kernel<false, false>);
+  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
+  auto k = next ? (rag ? (two ? big_step_kernel<true, true, 2> : big_step_kernel<true, true, 4>)
+                       : (two ? big_step_kernel<true, false, 2> : big_step_kernel<true, false, 4>))
+                : (rag ? (two ? big_step_kernel<false, true, 2> : big_step_kernel<false, true, 4>)
+                       : (two ? big_step_kernel<false, false, 2> : big_step_kernel<false, false, 4>));
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_step(const StepParams& p, hipStream_t s) {
-  auto k = (p.d % kColBlk) ? asss_big_step_kernel<true> : asss_big_step_kernel<false>;
+  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
+  auto k = rag ? (two ? asss_big_step_kernel<true, 2> : asss_big_step_kernel<true, 4>)
+               : (two ? asss_big_step_kernel<false, 2> : asss_big_step_kernel<false, 4>);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_pnx(const PnxParams& p, hipStream_t s) {
-  auto k = (p.d % kColBlk) ? big_pnx_kernel<true> : big_pnx_kernel<false>;
+  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
+  auto k = rag ? (two ? big_pnx_kernel<true, 2> : big_pnx_kernel<true, 4>)
+               : (two ? big_pnx_kernel<false, 2> : big_pnx_kernel<false, 4>);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s) {
-  auto k = (p.d % kColBlk) ? asss_big_pnx_kernel<true> : asss_big_pnx_kernel<false>;
+  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
+  auto k = rag ? (two ? asss_big_pnx_kernel<true, 2> : asss_big_pnx_kernel<true, 4>)
+               : (two ? asss_big_pnx_kernel<false, 2> : asss_big_pnx_kernel<false, 4>);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
