@@ -734,6 +734,10 @@ void orc_pooled_stats_k(const orc_cfg* cfg, int64_t C, int32_t i, int32_t K, con
                         const uint32_t* keys, const float* mu, const float* Lpacked, float lam,
                         float* z_out, float* pe_out, double* sums) {
   const int d = cfg->d;
+  if (d > ORC_DMAX && !orc_pooled_big(cfg)) { /* no pooled mode there (the library returns AMH_EINVAL) */
+    for (int64_t v = 0; v < d + packed_size(d) + 2; ++v) sums[v] = NAN;
+    return;
+  }
   if (orc_pooled_big(cfg) && d == 64) {
     orc_pooled_stats64_k(cfg, C, i, K, z, pe, keys, mu, Lpacked, lam, z_out, pe_out, sums);
     return;
@@ -854,6 +858,7 @@ int orc_pooled_update_k(const orc_cfg* cfg, const double* sums, int32_t K, int32
                         float* Lpacked, float* lam, float* asc, double* cov) {
   const int d = cfg->d;
   if (orc_pooled_big(cfg)) return orc_pooled_update_big(cfg, sums, K, i_, macc, mu, Lpacked, lam, asc, cov);
+  if (d > ORC_DMAX) return 0; /* no pooled mode at this d (see orc_pooled_stats_k) */
   const int64_t P = packed_size(d);
   const double N = sums[d + P + 1];
   const int32_t it = *i_;

@@ -92,3 +92,20 @@ def test_frozen_target_factor_keeps_target(orc):
     assert np.max(np.abs(zmean)) < 5.0
     ratio = out.var(0) / np.diag(Sigma)
     assert 0.75 < np.median(ratio) < 1.25
+
+
+def test_oracle_pooled_refuses_ragged_large_d(orc):
+    """The pooled mode has no d > 64 off the 32-multiples (the library's
+    amh_pooled_stats returns AMH_EINVAL); the oracle answers NaN sums and
+    leaves the shared state alone instead of running its d <= 64 arrays."""
+    from kernels_amd import PRNGKey
+    d, C = 100, 8
+    _, om, _ = _case(d)
+    st = orc.init(om, PRNGKey(0), C)
+    sh = orc.pooled_init_shared(d)
+    L0 = sh["L"].copy()
+    _, _, sums = orc.pooled_stats(om, 0, st.z, st.potential_energy, st.rng_key, sh["mu"], sh["L"],
+                                  float(sh["lam"][0]))
+    assert np.isnan(sums).all()
+    orc.pooled_update(om, sums, sh)
+    assert np.array_equal(sh["L"], L0)
