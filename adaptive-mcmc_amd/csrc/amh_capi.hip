@@ -116,6 +116,10 @@ int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d
       if (d < 1 || d > 16) { *why = "mixture needs 1 <= d <= 16"; return -1; }
       return d;
     }
+    case AMH_MODEL_EXTERNAL:
+      if (n_data < 0 || nip != 0) { *why = "external potential takes no data or iparams"; return -1; }
+      if (d < 1 || d > 64) { *why = "external potential needs 1 <= d <= 64"; return -1; }
+      return d;
     default:
       *why = "unknown model id";
       return -1;
@@ -271,6 +275,8 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
       amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model};
       e = amh::run_big_potential(q, (hipStream_t)stream);
     }
+  } else if (h->model_id == AMH_MODEL_EXTERNAL) {
+    e = amh::run_init_nopot(p, (hipStream_t)stream);  // pe0 = 0: the caller evaluates U(z0)
   } else if (amh::split_model(h->model_id, p.d)) {
     // pe0 = U(z0) from the lane-per-chain potential (bit-identical to the group one)
     e = amh::run_init_nopot(p, (hipStream_t)stream);
@@ -296,6 +302,8 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_step: no model bound");
   if (!state_ok(in) || !state_ok(out) || num_chains < 1 || n_steps < 0)
     return fail(h, AMH_EINVAL, "amh_step: bad arguments");
+  if (h->model_id == AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_step: an external potential runs through amh_propose / amh_step_external");
   if (n_steps == 0) {
     h->big_ready_C = -1;  // a kept proposal never survives a call it was not used in
     return AMH_OK;
@@ -420,6 +428,7 @@ int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* str
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_potential: null handle");
   if (!h->model_id) return fail(h, AMH_ENOMODEL, "amh_potential: no model bound");
   if (!z || !pe || n < 1) return fail(h, AMH_EINVAL, "amh_potential: bad arguments");
+  if (h->model_id == AMH_MODEL_EXTERNAL) return fail(h, AMH_EINVAL, "amh_potential: the potential is external");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential/hipSetDevice");
   amh::PotParams p{z, pe, n, h->cfg.dim, h->model, h->xpack};
@@ -427,6 +436,63 @@ int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* str
       : amh::split_model(h->model_id, p.d) ? amh::run_potential_lane(h->model_id, p, (hipStream_t)stream)
                                            : amh::run_potential(h->model_id, p, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_potential");
+  return AMH_OK;
+}
+
+// ------------------------------------------------- external potential --
+// AMH_MODEL_EXTERNAL: the split transition (amh_split.hip propose_kernel,
+// the step kernel with U(z') read from memory -- the diamonds path's two
+// launches) with the caller's U in between.
+static amh::StepParams ext_params(amh_handle* h, int64_t C, const amh_state* in, const amh_state* out) {
+  amh::StepParams p{};
+  p.in = *in;
+  p.out = *out;
+  p.C = C;
+  p.d = h->cfg.dim;
+  p.W = h->cfg.num_warmup;
+  p.a = h->cfg.lr_decay;
+  p.target = h->cfg.target_accept_prob;
+  p.eps = h->cfg.eps;
+  p.n_steps = 1;
+  p.thinning = 1;
+  p.gamma_tab = h->gamma_tab;
+  p.gamma_tab_n = amh::kGammaTab;
+  p.model = h->model;
+  return p;
+}
+
+int amh_propose(amh_handle* h, int64_t num_chains, const amh_state* in, float* zprop, void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_propose: null handle");
+  if (h->model_id != AMH_MODEL_EXTERNAL) return fail(h, AMH_EINVAL, "amh_propose: needs AMH_MODEL_EXTERNAL");
+  if (!state_ok(in) || !zprop || num_chains < 1) return fail(h, AMH_EINVAL, "amh_propose: bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_propose/hipSetDevice");
+  const amh::StepParams p = ext_params(h, num_chains, in, in);
+  e = amh::run_propose(p, zprop, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_propose");
+  return AMH_OK;
+}
+
+int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+                      const float* zprop, const float* pe_prop, float* zprop_next, const amh_collect* collect,
+                      void* stream) {
+  if (!h) return fail(nullptr, AMH_EINVAL, "amh_step_external: null handle");
+  if (h->model_id != AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_step_external: needs AMH_MODEL_EXTERNAL");
+  if (!state_ok(in) || !state_ok(out) || !zprop || !pe_prop || num_chains < 1)
+    return fail(h, AMH_EINVAL, "amh_step_external: bad arguments");
+  if (collect && collect->thinning != 1) return fail(h, AMH_EINVAL, "amh_step_external: thinning must be 1");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_step_external/hipSetDevice");
+  amh::StepParams p = ext_params(h, num_chains, in, out);
+  p.col_z = collect ? collect->z : nullptr;
+  p.col_pe = collect ? collect->potential_energy : nullptr;
+  p.accept_count = collect ? collect->accept_count : nullptr;
+  p.ext_z = zprop;
+  p.ext_pe = pe_prop;
+  p.xprop_next = zprop_next;
+  e = amh::run_step_ext(p, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, "amh_step_external");
   return AMH_OK;
 }
 
@@ -440,6 +506,8 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
     return fail(h, AMH_EINVAL, "amh_sample_pnx: bad arguments");
   if (h->cfg.dim > 64 && !amh::big_model(h->model_id, h->cfg.dim))
     return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 needs the dense Gaussian (d <= 256)");
+  if (h->model_id == AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_sample_pnx: the frozen kernel needs a device potential (not external)");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
   amh::PnxParams p{};
@@ -481,6 +549,8 @@ int amh_asss_step(amh_handle* h, int64_t num_chains, const amh_state* in, const 
   const bool big = amh::big_model(h->model_id, h->cfg.dim);
   if (h->cfg.dim > 64 && !big)
     return fail(h, AMH_EINVAL, "amh_asss_step: dim must be <= 64, or a dense Gaussian up to 256");
+  if (h->model_id == AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_asss_step: the slice sampler needs a device potential (not external)");
   if (collect && collect->thinning < 1) return fail(h, AMH_EINVAL, "amh_asss_step: thinning must be >= 1");
   if (n_steps == 0) return AMH_OK;
   hipError_t e = hipSetDevice(h->device);
@@ -533,6 +603,8 @@ int amh_asss_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, in
   const bool big = amh::big_model(h->model_id, h->cfg.dim);
   if (h->cfg.dim > 64 && !big)
     return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: dim must be <= 64, or a dense Gaussian up to 256");
+  if (h->model_id == AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_asss_sample_pnx: the slice sampler needs a device potential (not external)");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_asss_sample_pnx/hipSetDevice");
   amh::AsssPnxParams p{};
@@ -658,6 +730,8 @@ static int pooled_stats_impl(amh_handle* h, int64_t num_chains, const amh_pooled
   const int d = h->cfg.dim;
   const bool big = amh::pooled_big_model(h->model_id, d);
   if (d > 64 && !big) return fail(h, AMH_EINVAL, "amh_pooled_stats: d > 64 needs d % 32 == 0 in the pooled mode");
+  if (h->model_id == AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_pooled_stats: the pooled mode needs a device potential (not external)");
   const int cpw = amh::pooled_cpw(num_chains);
   const int64_t chunk = (int64_t)amh::kPoolWaves * cpw;
   const int64_t n_chunks = big ? amh::pooled_big_chunks(num_chains, d) : (num_chains + chunk - 1) / chunk;

@@ -1826,12 +1826,14 @@ hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s) {
 // split path (amh_split.hip): the step kernel with U(z') read from p.ext_pe,
 // and init without the potential (filled by the batched potential kernel)
 hipError_t run_step_ext(const StepParams& p, hipStream_t s) {
-  if (p.d < 1 || p.d > 32 || p.n_steps != 1 || p.ext_pe == nullptr) return hipErrorInvalidValue;
+  if (p.d < 1 || p.d > 64 || p.n_steps != 1 || p.ext_pe == nullptr) return hipErrorInvalidValue;
   if (p.d == kDiamondsD) return launch_step<32, ExtPotM, false, kDiamondsD>(p, s);
+  if (p.d > 32) return launch_step<64, ExtPotM, false>(p, s);  // the external potential's 33..64
   return launch_step<32, ExtPotM, false>(p, s);
 }
 hipError_t run_init_nopot(const InitParams& p, hipStream_t s) {
-  if (p.d < 1 || p.d > 32) return hipErrorInvalidValue;
+  if (p.d < 1 || p.d > 64) return hipErrorInvalidValue;
+  if (p.d > 32) return launch_init<64, ExtPotM, false>(p, s);
   return launch_init<32, ExtPotM, false>(p, s);
 }
 

@@ -401,7 +401,13 @@ hipError_t run_diamonds_pack(const ModelArgs& m, float* xp, hipStream_t s) {
 
 // ---------------------------------------------------------------- launchers --
 hipError_t run_propose(const StepParams& p, float* xprop, hipStream_t s) {
-  if (p.d < 1 || p.d > 32) return hipErrorInvalidValue;
+  if (p.d < 1 || p.d > 64) return hipErrorInvalidValue;
+  if (p.d > 32) {  // the external potential's 33 <= d <= 64: one chain per wave
+    int64_t blocks = (p.C + kBlock / 64 - 1) / (kBlock / 64);
+    if (blocks > 256 * 32) blocks = 256 * 32;
+    hipLaunchKernelGGL(propose_kernel<64>, dim3((unsigned)(blocks > 0 ? blocks : 1)), dim3(kBlock), 0, s, p, xprop);
+    return hipGetLastError();
+  }
   const int64_t n_items = (p.C + Geo<32>::CPW - 1) / Geo<32>::CPW;
   int64_t blocks = (n_items + kBlock / 64 - 1) / (kBlock / 64);
   if (blocks > 256 * 32) blocks = 256 * 32;

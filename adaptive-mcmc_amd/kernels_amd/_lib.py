@@ -22,6 +22,7 @@ AMH_MODEL_KIDIQ = 3
 AMH_MODEL_DIAMONDS = 4
 AMH_MODEL_DIAMONDS_SS = 5
 AMH_MODEL_MIXTURE = 6
+AMH_MODEL_EXTERNAL = 7  # the caller's potential (amh_propose / amh_step_external)
 AMH_STEP_PROPOSAL_READY = 1
 AMH_STEP_KEEP_PROPOSAL = 2
 
@@ -31,7 +32,8 @@ EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bi
            "amh_pooled_stats", "amh_pooled_update", "amh_pooled_step", "amh_pooled_stats_k", "amh_pooled_update_k",
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
-           "amh_normals", "amh_sinkhorn_lse", "amh_check_device", "amh_pooled_allreduce")
+           "amh_normals", "amh_sinkhorn_lse", "amh_check_device", "amh_pooled_allreduce", "amh_propose",
+           "amh_step_external")
 
 
 class AmhConfig(ctypes.Structure):
@@ -97,6 +99,11 @@ def lib():
                                 ctypes.POINTER(AmhCollect), P]
     L.amh_asss_step.restype = ctypes.c_int
     L.amh_asss_sample_pnx.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, I64, P, P, I32, P, P]
+    L.amh_propose.argtypes = [P, I64, ctypes.POINTER(AmhState), P, P]
+    L.amh_propose.restype = ctypes.c_int
+    L.amh_step_external.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), P, P, P,
+                                    ctypes.POINTER(AmhCollect), P]
+    L.amh_step_external.restype = ctypes.c_int
     L.amh_asss_sample_pnx.restype = ctypes.c_int
     L.amh_kernel_sum_scratch.argtypes = [I64, I64]
     L.amh_kernel_sum_scratch.restype = I64

@@ -93,8 +93,11 @@ class ARWMH:
     ----------
     model : posteriors.Model, optional
         Registry model; its data are passed as `model_kwargs` to `init`.
-    potential_fn : posteriors.Gaussian, optional
-        Device potential (raw potential_fn plug-in).  Exactly one of `model`
+    potential_fn : posteriors.Gaussian / Mixture, or any callable, optional
+        Device potential (raw potential_fn plug-in), fused into the kernel;
+        any other callable (a batched torch function z [n, d] -> U [n], or a
+        posteriors.TorchPotential) runs between the kernel's proposal and
+        step launches (AMH_MODEL_EXTERNAL, d <= 64).  Exactly one of `model`
         and `potential_fn` must be given.
     lr_decay : float, gamma_n = 1 / n^lr_decay (default 2/3).
     target_accept_prob : float (default 0.234).
@@ -112,8 +115,11 @@ class ARWMH:
                  init_strategy=init_to_uniform, num_chains=None, device=None, chain_offset=0):
         if not (model is None) ^ (potential_fn is None):
             raise ValueError("Only one of `model` or `potential_fn` must be specified.")
-        if potential_fn is not None and callable(potential_fn) and not hasattr(potential_fn, "model_id"):
-            raise TypeError("potential_fn must be a device potential from `posteriors` (e.g. posteriors.gaussian)")
+        if potential_fn is not None and not hasattr(potential_fn, "model_id"):
+            if not callable(potential_fn):
+                raise TypeError("potential_fn must be callable")
+            import posteriors as _P
+            potential_fn = _P.TorchPotential(potential_fn)  # dim from init_params
         self._model = model
         self._potential_fn = potential_fn
         self._lr_decay = lr_decay
@@ -192,6 +198,9 @@ class ARWMH:
             raise ValueError("Valid value of `init_params` must be provided with `potential_fn`.")
         device_index = _device_index(self._device)
         device = torch.device("cuda", device_index)
+        if self._external() and self._potential_fn.dim is None:
+            x = init_params.cpu() if hasattr(init_params, "cpu") else np.asarray(init_params)
+            self._potential_fn.dim = int(np.asarray(x).shape[-1]) if np.ndim(x) else 1
         self._bind(int(num_warmup), dict(model_kwargs or {}), device_index)
         d = self._dim
         iz = None
@@ -210,6 +219,10 @@ class ARWMH:
                                            ctypes_state(self, state), _lib.stream_ptr(device_index)),
                        self._handle.h)
         self.accept_count = torch.zeros(C, dtype=torch.int32, device=device)
+        if self._external():  # pe0 = U(z0) by the caller's potential (amh_init left 0)
+            with torch.cuda.device(device_index):
+                state.potential_energy.copy_(self._potential_fn.evaluate(state.z))
+            self._zprop = None
         if self._model is not None:
             mk = self._model_kwargs
             self._postprocess_fn = lambda *a, **k: (lambda z: self._model.postprocess(z, mk))
@@ -264,9 +277,37 @@ class ARWMH:
         return (state.i, state.z, state.potential_energy, state.mean_accept_prob, a.loc, a.scale,
                 a.log_step_size, state.as_change, state.rng_key)
 
+    def _external(self) -> bool:
+        return self._potential_fn is not None and self._potential_fn.model_id == _lib.AMH_MODEL_EXTERNAL
+
+    def _launch_external(self, sin, sout, n_steps, collect):
+        """AMH_MODEL_EXTERNAL: per transition amh_step_external with the
+        caller's U of the proposals, which the previous launch formed (the
+        first by amh_propose).  Collection as the fused launch (thinning)."""
+        cz, cp, thin = collect if collect is not None else (None, None, 1)
+        C, d, dev = sin.z.shape[0], self._dim, sin.z.device
+        zp = torch.empty(C, d, dtype=torch.float32, device=dev)
+        lib = _lib.lib()
+        acc = self.accept_count.data_ptr() if self.accept_count is not None else None
+        with torch.cuda.device(dev.index):
+            st = _lib.stream_ptr(dev.index)
+            _lib.check(lib.amh_propose(self._handle.h, C, ctypes_state(self, sin), _lib.ptr(zp), st), self._handle.h)
+            for t in range(int(n_steps)):
+                src = sin if t == 0 else sout
+                pe = self._potential_fn.evaluate(zp)
+                keep = (t + 1) % thin == 0
+                k = t // thin
+                col = _lib.AmhCollect(cz[k].data_ptr() if (keep and cz is not None) else None,
+                                      cp[k].data_ptr() if (keep and cp is not None) else None, acc, 1)
+                nxt = _lib.ptr(zp) if t + 1 < n_steps else None
+                _lib.check(lib.amh_step_external(self._handle.h, C, ctypes_state(self, src), ctypes_state(self, sout),
+                                                 _lib.ptr(zp), _lib.ptr(pe), nxt, col, st), self._handle.h)
+
     def _launch(self, sin, sout, n_steps, collect):
         if int(n_steps) == 0:
             return  # no launch: the chained proposal (if any) stays with the tensors it was made for
+        if self._external():
+            return self._launch_external(sin, sout, n_steps, collect)
         cz, cp, thin = collect if collect is not None else (None, None, 1)
         col = _lib.AmhCollect(cz.data_ptr() if cz is not None else None,
                               cp.data_ptr() if cp is not None else None,
@@ -322,6 +363,8 @@ class ARWMH:
     def potential(self, z: torch.Tensor) -> torch.Tensor:
         """potential_fn(z) for a batch of flat points [n, d] (device)."""
         _lib.require_gpu(z)
+        if self._external():
+            return self._potential_fn.evaluate(z.to(torch.float32).contiguous().reshape(-1, self._dim))
         z = z.to(torch.float32).contiguous().reshape(-1, self._dim)
         pe = torch.empty(z.shape[0], dtype=torch.float32, device=z.device)
         with torch.cuda.device(z.device.index):

@@ -300,6 +300,40 @@ def notebook_mixture() -> Mixture:
     return mixture([0.5, 0.5], [-1.0, 1.0], [0.1, 0.1])
 
 
+# ------------------------------------------------------------------ external --
+@dataclass
+class TorchPotential:
+    """Any potential the caller writes (arwmh.py:69-70: `potential_fn` is an
+    arbitrary callable there): `fn` maps a device batch z [n, d] float32 to
+    U(z) [n] (-log density, NaN allowed: it rejects).  ARWMH runs the rest
+    of the transition in its kernels around it (include/amh.h
+    AMH_MODEL_EXTERNAL: amh_propose, fn, amh_step_external), 1 <= d <= 64.
+    `dim` may be left None: init() takes it from init_params."""
+    fn: Callable
+    dim: int = None
+    model_id: int = field(default=_lib.AMH_MODEL_EXTERNAL, init=False)
+    name: str = field(default="external", init=False)
+
+    def pack(self, device) -> Tuple[torch.Tensor, Tuple[int, ...]]:
+        return torch.zeros(1, dtype=torch.float32, device=device), ()  # no data (the library reads none)
+
+    def evaluate(self, z: torch.Tensor) -> torch.Tensor:
+        u = self.fn(z)
+        u = torch.as_tensor(u, device=z.device).to(torch.float32).reshape(-1)
+        if u.shape[0] != z.shape[0]:
+            raise ValueError(f"potential_fn returned {tuple(u.shape)} values for {z.shape[0]} points (one each)")
+        return u.contiguous()
+
+    def __call__(self, z):
+        return self.fn(z)
+
+
+def torch_potential(fn: Callable, dim: int = None) -> TorchPotential:
+    if dim is not None and not 1 <= int(dim) <= 64:
+        raise ValueError("an external potential supports 1 <= dim <= 64")
+    return TorchPotential(fn, None if dim is None else int(dim))
+
+
 REGISTRY = {
     "eight_schools": eight_schools,
     "eight_schools_noncentered": eight_schools,

@@ -62,10 +62,15 @@ enum {
   AMH_MODEL_DIAMONDS_SS = 5,   /* diamonds through float64 sufficient statistics, passed as
                                   2 floats each: [N, ybar, A, sT, t (Kc), sx (Kc), Gm (Kc*Kc)],
                                   n_data = 2 (4 + 2 Kc + Kc^2), iparams {N, K}, 3 <= d <= 32 */
-  AMH_MODEL_MIXTURE = 6        /* K-component univariate normal mixture on every coordinate
+  AMH_MODEL_MIXTURE = 6,       /* K-component univariate normal mixture on every coordinate
                                   (asumptions_check.ipynb cells 61-62): data [c (K) | m (K) |
                                   s (K)], c_k = log w_k - log(sqrt(2 pi) s_k); iparams {K},
                                   1 <= K <= 8, n_data = 3 K, 1 <= d <= 16 */
+  AMH_MODEL_EXTERNAL = 7       /* the caller's potential (arwmh.py:69-70 potential_fn, any
+                                  callable): the library never evaluates U; amh_init leaves
+                                  pe0 = 0 for the caller to fill, transitions run through
+                                  amh_propose / amh_step_external; data ignored (non-null,
+                                  n_data >= 0, no iparams), 1 <= d <= 64 */
 };
 
 typedef struct amh_config {
@@ -148,6 +153,22 @@ int amh_step(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_s
 enum { AMH_STEP_PROPOSAL_READY = 1, AMH_STEP_KEEP_PROPOSAL = 2 };
 int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
                      int32_t n_steps, const amh_collect* collect, int32_t flags, void* stream);
+
+/* AMH_MODEL_EXTERNAL: ARWMH.sample (arwmh.py:140-207) with U evaluated by the
+ * caller between two launches.  amh_propose writes every chain's proposal
+ * z' = z + (L e^lam + eps I) xi (arwmh.py:162-167, the step stream at in.i)
+ * to zprop[C][d].  amh_step_external then runs the rest of the transition
+ * (accept with pe_prop[C] = U(zprop), NaN -> +inf as arwmh.py:171; the
+ * schedule, mean, rank-one update and step size) from `in` to `out`; with
+ * zprop_next non-null it also writes the NEXT transition's proposals (from
+ * `out`, in the same pass over the factor; zprop_next may equal zprop), so a
+ * chain of transitions is propose once, then {U; step_external}.  collect:
+ * z / potential_energy after the transition (thinning 1) and accept_count.
+ * `in` and `out` may alias.  Same bits as the fused kernels with the same U. */
+int amh_propose(amh_handle* h, int64_t num_chains, const amh_state* in, float* zprop, void* stream);
+int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
+                      const float* zprop, const float* pe_prop, float* zprop_next, const amh_collect* collect,
+                      void* stream);
 
 /* potential_fn(z) for n points: pe[n] from z[n][d] (arwmh.py:121). */
 int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* stream);

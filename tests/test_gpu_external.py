@@ -1,0 +1,112 @@
+"""The external-potential path (AMH_MODEL_EXTERNAL: amh_propose, the
+caller's U, amh_step_external; arwmh.py:69-70's arbitrary potential_fn) on
+the GPU.  With U = the library's own Gaussian potential (amh_potential,
+bit-identical to the oracle's) the transitions must equal orc_step bit for
+bit -- single launches, in-place multi-step runs and thinned collection --
+at d where the fused Gaussian kernel's lane group is the external path's
+(32 for 17 <= d <= 32, 64 above; d = 64's fused kernel is the step64
+specialisation, bit-identical to the generic one).  A potential written in torch samples its target."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from helpers import assert_state_bitequal, make_case
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(d, C, gpu, orc, W=4, seed=0):
+    from kernels_amd import ARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", d)
+    z0 = np.random.default_rng(seed).uniform(-2, 2, size=(C, d)).astype(np.float32)
+    kg = ARWMH(num_chains=8, **kw)  # the registry kernel, for its potential only
+    kg.init(PRNGKey(1), 0, torch.as_tensor(z0[:8]), (), mk)
+    ke = ARWMH(potential_fn=lambda z: kg.potential(z), num_chains=C)
+    st = ke.init(PRNGKey(seed), W, torch.as_tensor(z0), (), {})
+    ost = orc.init(om, PRNGKey(seed), C, init_z=z0)
+    torch.cuda.synchronize()
+    return ke, st, om, ost
+
+
+@pytest.mark.parametrize("d,C", [(24, 333), (32, 200), (17, 65), (48, 130), (64, 77)])
+def test_external_matches_oracle_bitexact(d, C, gpu, orc):
+    ke, st, om, ost = _pair(d, C, gpu, orc)
+    assert_state_bitequal(st, ost, f"d={d} init")
+    acc = np.zeros(C, np.int32)
+    for t in range(8):  # crosses gamma_1 = 1 (keep L) and the warmup reset at W + 1
+        st = ke.sample(st, (), {})
+        orc.step(om, ost, 1, num_warmup=4, accept_count=acc)
+        torch.cuda.synchronize()
+        assert_state_bitequal(st, ost, f"d={d} step {t}")
+    np.testing.assert_array_equal(ke.accept_count.cpu().numpy(), acc)
+    # every external transition is its own launch (the state goes through
+    # HBM, L = U diag(dl) stored and re-read), so the oracle runs one step per
+    # call -- its fused n-step call keeps U across steps, as the fused kernels
+    ke.sample_(st, 5)  # in place: the chained proposals of amh_step_external
+    for _ in range(5):
+        orc.step(om, ost, 1, num_warmup=4)
+    torch.cuda.synchronize()
+    assert_state_bitequal(st, ost, f"d={d} in-place")
+    st2, cz, cp = ke.run(st, 6, thinning=3, collect_z=True, collect_pe=True)
+    ozs, ops = [], []
+    for _ in range(6):
+        orc.step(om, ost, 1, num_warmup=4)
+        ozs.append(ost.z.copy())
+        ops.append(ost.potential_energy.copy())
+    torch.cuda.synchronize()
+    assert_state_bitequal(st2, ost, f"d={d} run")
+    np.testing.assert_array_equal(cz.cpu().numpy().view(np.uint32), np.stack(ozs)[2::3].view(np.uint32))
+    np.testing.assert_array_equal(cp.cpu().numpy().view(np.uint32), np.stack(ops)[2::3].view(np.uint32))
+
+
+def test_torch_potential_samples_target(gpu):
+    """U written in torch (a correlated 3-D Gaussian): after adaptation the
+    chains' moments are the target's and acceptance is near 0.234."""
+    from kernels_amd import ARWMH, PRNGKey
+    S = torch.tensor([[1.0, 0.5, 0.0], [0.5, 2.0, -0.3], [0.0, -0.3, 0.5]], dtype=torch.float64)
+    Pm = torch.linalg.inv(S).to(torch.float32).cuda()
+    m = torch.tensor([1.0, -2.0, 0.5], device="cuda")
+
+    def U(z):
+        x = z - m
+        return 0.5 * ((x @ Pm) * x).sum(-1)
+
+    C = 4096
+    k = ARWMH(potential_fn=U, num_chains=C)
+    st = k.init(PRNGKey(3), 0, torch.rand(C, 3) * 4 - 2, (), {})
+    k.sample_(st, 1500)
+    st, cz, _ = k.run(st, 400, thinning=20, collect_z=True)
+    z = cz.reshape(-1, 3).double().cpu()
+    np.testing.assert_allclose(z.mean(0).numpy(), m.cpu().numpy(), atol=0.05)
+    np.testing.assert_allclose(torch.cov(z.T).numpy(), S.numpy(), atol=0.08)
+    assert abs(float(st.mean_accept_prob.mean()) - 0.234) < 0.03
+    np.testing.assert_allclose(st.potential_energy.cpu().numpy(), U(st.z).cpu().numpy(), rtol=1e-6, atol=1e-6)
+
+
+def test_external_limits(gpu):
+    """What the external path does not take: sample_Pnx and ASSS (the
+    frozen / slice kernels evaluate U inside), d > 64, a potential that
+    returns the wrong number of values; NaN rejects (arwmh.py:171)."""
+    from kernels_amd import ARWMH, ASSS, PRNGKey
+    from kernels_amd._lib import AmhError
+    U = lambda z: 0.5 * (z * z).sum(-1)  # noqa: E731
+    k = ARWMH(potential_fn=U, num_chains=64)
+    st = k.init(PRNGKey(0), 0, torch.zeros(64, 4), (), {})
+    with pytest.raises(AmhError, match="device potential"):
+        k.sample_Pnx(PRNGKey(1), torch.zeros(2, 4), (st.adapt_state.loc[0], st.adapt_state.scale[0],
+                                                     st.adapt_state.log_step_size[0]), n=1, n_samples=4)
+    with pytest.raises(AmhError, match="device potential"):
+        a = ASSS(potential_fn=U, num_chains=64)
+        a.sample(a.init(PRNGKey(0), 0, torch.zeros(64, 4), (), {}))
+    with pytest.raises(AmhError, match="1 <= d <= 64"):
+        ARWMH(potential_fn=U, num_chains=8).init(PRNGKey(0), 0, torch.zeros(8, 70), (), {})
+    bad = ARWMH(potential_fn=lambda z: z.sum(), num_chains=8)
+    with pytest.raises(ValueError, match="one each"):
+        bad.init(PRNGKey(0), 0, torch.zeros(8, 4), (), {})
+    nan = ARWMH(potential_fn=lambda z: torch.where(z[:, 0] > 0, torch.nan, 0.5 * (z * z).sum(-1)), num_chains=256)
+    s = nan.init(PRNGKey(2), 0, -torch.ones(256, 2), (), {})
+    nan.sample_(s, 200)
+    assert bool((s.z[:, 0] <= 0).all())  # every proposal into the NaN half was rejected
+    assert math.isfinite(float(s.potential_energy.max()))

@@ -109,3 +109,21 @@ def test_oracle_pooled_refuses_ragged_large_d(orc):
     assert np.isnan(sums).all()
     orc.pooled_update(om, sums, sh)
     assert np.array_equal(sh["L"], L0)
+
+
+def test_callable_potential_becomes_external():
+    """arwmh.py:69-70 takes any callable as potential_fn: a callable without
+    a registry model id is wrapped as posteriors.TorchPotential (the
+    AMH_MODEL_EXTERNAL path, dim from init_params), still XOR with model."""
+    import posteriors as P
+    from kernels_amd import ARWMH
+    from kernels_amd import _lib
+    k = ARWMH(potential_fn=lambda z: (z * z).sum(-1))
+    assert isinstance(k._potential_fn, P.TorchPotential) and k._potential_fn.dim is None
+    assert k._potential_fn.model_id == _lib.AMH_MODEL_EXTERNAL == 7
+    with pytest.raises(ValueError):
+        ARWMH(model=P.eight_schools, potential_fn=lambda z: z)
+    with pytest.raises(TypeError):
+        ARWMH(potential_fn=3.0)
+    with pytest.raises(ValueError):
+        P.torch_potential(lambda z: z, dim=65)
