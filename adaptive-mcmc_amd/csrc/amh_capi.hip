@@ -28,6 +28,8 @@ struct amh_handle {
   float* split_buf = nullptr;  // split path: proposals [C][d] then U(z') [C] (scratch)
   int64_t big_ready_C = -1;    // d > 64: split_buf holds the next proposal of the last output state (C chains)
   amh_state big_ready_out{};   // ... and that output state's buffers: READY is honoured only for these
+  int64_t ext_ready_C = -1;    // external potential, d > 64: split_buf holds the solves (wa, wr, dg) of
+  amh_state ext_ready_in{};    // the proposals formed from this state (amh_propose / amh_step_external)
   size_t split_bytes = 0;
   float* upd_buf = nullptr;    // pooled d > 64: Sigma' / L' staging (4-row-aligned layout) + ok flag
   size_t upd_bytes = 0;
@@ -118,7 +120,7 @@ int expected_dim(int model_id, int64_t n_data, const int64_t* ip, int nip, int d
     }
     case AMH_MODEL_EXTERNAL:
       if (n_data < 0 || nip != 0) { *why = "external potential takes no data or iparams"; return -1; }
-      if (d < 1 || d > 64) { *why = "external potential needs 1 <= d <= 64"; return -1; }
+      if (d < 1 || d > 256) { *why = "external potential needs 1 <= d <= 256"; return -1; }
       return d;
     default:
       *why = "unknown model id";
@@ -215,8 +217,8 @@ int amh_bind_model(amh_handle* h, int32_t model_id, const float* data, int64_t n
   if (dm != h->cfg.dim)
     return fail(h, AMH_EINVAL, "amh_bind_model: model dimension " + std::to_string(dm) + " != config dim " +
                                    std::to_string(h->cfg.dim));
-  if (dm > 64 && !amh::big_model(model_id, dm))
-    return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model (d <= 256)");
+  if (dm > 64 && !amh::big_model(model_id, dm) && model_id != AMH_MODEL_EXTERNAL)
+    return fail(h, AMH_EINVAL, "amh_bind_model: d > 64 needs the Gaussian model or an external potential (d <= 256)");
   // the handle's device for everything below (the caller -- Handle.bind_model --
   // holds it current and restores its own afterwards)
   hipError_t e = hipSetDevice(h->device);
@@ -258,6 +260,7 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
   if (!key || !state_ok(out) || num_chains < 1 || chain_offset < 0)
     return fail(h, AMH_EINVAL, "amh_init: bad arguments");
   h->big_ready_C = -1;  // a kept proposal belongs to a state this call may overwrite
+  h->ext_ready_C = -1;
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_init/hipSetDevice");
   amh::InitParams p{};
@@ -269,7 +272,9 @@ int amh_init(amh_handle* h, const uint32_t key[2], int64_t chain_offset, int64_t
   p.key1 = key[1];
   p.init_z = init_z;
   p.model = h->model;
-  if (amh::big_model(h->model_id, p.d)) {
+  if (h->model_id == AMH_MODEL_EXTERNAL && p.d > 64) {
+    e = amh::run_big_init(p, (hipStream_t)stream);  // pe0 = 0: the caller evaluates U(z0)
+  } else if (amh::big_model(h->model_id, p.d)) {
     e = amh::run_big_init(p, (hipStream_t)stream);
     if (e == hipSuccess) {
       amh::PotParams q{out->z, out->potential_energy, num_chains, p.d, h->model};
@@ -461,12 +466,52 @@ static amh::StepParams ext_params(amh_handle* h, int64_t C, const amh_state* in,
   return p;
 }
 
+// d > 64: big_propose_kernel / big_step_kernel with the caller's U(z'); the
+// proposals live in the caller's zprop, the solves (wa, wr) and the diagonal
+// in the handle's scratch, tied to the state they were formed from
+static int ext_big_params(amh_handle* h, int64_t C, const amh_state* in, const amh_state* out, float* zprop,
+                          void* stream, amh::BigParams* q) {
+  const int d = h->cfg.dim;
+  const size_t need = (size_t)C * (size_t)(3 * d) * sizeof(float);
+  const bool grown = need > h->split_bytes;
+  int rc = grow(h, &h->split_buf, &h->split_bytes, need, stream, "amh_propose/hipMalloc");
+  if (rc != AMH_OK) return rc;
+  if (grown) h->ext_ready_C = -1;
+  h->big_ready_C = -1;  // the scratch now holds the external path's solves
+  *q = amh::BigParams{};
+  q->in = *in;
+  q->out = *out;
+  q->C = C;
+  q->d = d;
+  q->W = h->cfg.num_warmup;
+  q->a = h->cfg.lr_decay;
+  q->target = h->cfg.target_accept_prob;
+  q->eps = h->cfg.eps;
+  q->gamma_tab = h->gamma_tab;
+  q->gamma_tab_n = amh::kGammaTab;
+  q->xprop = zprop;
+  q->wa = h->split_buf;
+  q->wr = q->wa + (size_t)C * d;
+  q->dg = q->wr + (size_t)C * d;
+  return AMH_OK;
+}
+
 int amh_propose(amh_handle* h, int64_t num_chains, const amh_state* in, float* zprop, void* stream) {
   if (!h) return fail(nullptr, AMH_EINVAL, "amh_propose: null handle");
   if (h->model_id != AMH_MODEL_EXTERNAL) return fail(h, AMH_EINVAL, "amh_propose: needs AMH_MODEL_EXTERNAL");
   if (!state_ok(in) || !zprop || num_chains < 1) return fail(h, AMH_EINVAL, "amh_propose: bad arguments");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_propose/hipSetDevice");
+  if (h->cfg.dim > 64) {
+    amh::BigParams q;
+    int rc = ext_big_params(h, num_chains, in, in, zprop, stream, &q);
+    if (rc != AMH_OK) return rc;
+    e = amh::run_big_propose(q, (hipStream_t)stream);
+    if (e != hipSuccess) return hip_fail(h, e, "amh_propose(d > 64)");
+    h->ext_ready_C = num_chains;
+    h->ext_ready_in = *in;
+    return AMH_OK;
+  }
   const amh::StepParams p = ext_params(h, num_chains, in, in);
   e = amh::run_propose(p, zprop, (hipStream_t)stream);
   if (e != hipSuccess) return hip_fail(h, e, "amh_propose");
@@ -484,6 +529,29 @@ int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, co
   if (collect && collect->thinning != 1) return fail(h, AMH_EINVAL, "amh_step_external: thinning must be 1");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_step_external/hipSetDevice");
+  if (h->cfg.dim > 64) {
+    // the step pass reads the solves amh_propose (or the previous step) formed
+    // for exactly this state, and writes the next proposals in place
+    if (h->ext_ready_C != num_chains || !same_buffers(*in, h->ext_ready_in))
+      return fail(h, AMH_EINVAL, "amh_step_external: d > 64 needs the proposals of this state (amh_propose first)");
+    if (zprop_next && zprop_next != zprop)
+      return fail(h, AMH_EINVAL, "amh_step_external: d > 64 forms the next proposals in place (zprop_next == zprop)");
+    amh::BigParams q;
+    int rc = ext_big_params(h, num_chains, in, out, const_cast<float*>(zprop), stream, &q);
+    if (rc != AMH_OK) return rc;
+    q.pep = pe_prop;
+    q.accept_count = collect ? collect->accept_count : nullptr;
+    q.col_z = collect ? collect->z : nullptr;
+    q.col_pe = collect ? collect->potential_energy : nullptr;
+    h->ext_ready_C = -1;
+    e = amh::run_big_step(q, (hipStream_t)stream, zprop_next != nullptr);
+    if (e != hipSuccess) return hip_fail(h, e, "amh_step_external(d > 64)");
+    if (zprop_next) {
+      h->ext_ready_C = num_chains;
+      h->ext_ready_in = *out;
+    }
+    return AMH_OK;
+  }
   amh::StepParams p = ext_params(h, num_chains, in, out);
   p.col_z = collect ? collect->z : nullptr;
   p.col_pe = collect ? collect->potential_energy : nullptr;

@@ -97,7 +97,7 @@ class ARWMH:
         Device potential (raw potential_fn plug-in), fused into the kernel;
         any other callable (a batched torch function z [n, d] -> U [n], or a
         posteriors.TorchPotential) runs between the kernel's proposal and
-        step launches (AMH_MODEL_EXTERNAL, d <= 64).  Exactly one of `model`
+        step launches (AMH_MODEL_EXTERNAL, d <= 256).  Exactly one of `model`
         and `potential_fn` must be given.
     lr_decay : float, gamma_n = 1 / n^lr_decay (default 2/3).
     target_accept_prob : float (default 0.234).

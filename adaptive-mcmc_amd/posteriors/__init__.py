@@ -307,7 +307,7 @@ class TorchPotential:
     arbitrary callable there): `fn` maps a device batch z [n, d] float32 to
     U(z) [n] (-log density, NaN allowed: it rejects).  ARWMH runs the rest
     of the transition in its kernels around it (include/amh.h
-    AMH_MODEL_EXTERNAL: amh_propose, fn, amh_step_external), 1 <= d <= 64.
+    AMH_MODEL_EXTERNAL: amh_propose, fn, amh_step_external), 1 <= d <= 256.
     `dim` may be left None: init() takes it from init_params."""
     fn: Callable
     dim: int = None
@@ -329,8 +329,8 @@ class TorchPotential:
 
 
 def torch_potential(fn: Callable, dim: int = None) -> TorchPotential:
-    if dim is not None and not 1 <= int(dim) <= 64:
-        raise ValueError("an external potential supports 1 <= dim <= 64")
+    if dim is not None and not 1 <= int(dim) <= 256:
+        raise ValueError("an external potential supports 1 <= dim <= 256")
     return TorchPotential(fn, None if dim is None else int(dim))
 
 

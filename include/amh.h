@@ -70,7 +70,7 @@ enum {
                                   callable): the library never evaluates U; amh_init leaves
                                   pe0 = 0 for the caller to fill, transitions run through
                                   amh_propose / amh_step_external; data ignored (non-null,
-                                  n_data >= 0, no iparams), 1 <= d <= 64 */
+                                  n_data >= 0, no iparams), 1 <= d <= 256 */
 };
 
 typedef struct amh_config {
@@ -164,7 +164,10 @@ int amh_step_chained(amh_handle* h, int64_t num_chains, const amh_state* in, con
  * `out`, in the same pass over the factor; zprop_next may equal zprop), so a
  * chain of transitions is propose once, then {U; step_external}.  collect:
  * z / potential_energy after the transition (thinning 1) and accept_count.
- * `in` and `out` may alias.  Same bits as the fused kernels with the same U. */
+ * `in` and `out` may alias.  Same bits as the fused kernels with the same U.
+ * d > 64: the solves of the proposals stay in the handle, so amh_step_external
+ * takes only the state the last amh_propose / amh_step_external formed them
+ * from, and zprop_next must be null or zprop (AMH_EINVAL otherwise). */
 int amh_propose(amh_handle* h, int64_t num_chains, const amh_state* in, float* zprop, void* stream);
 int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, const amh_state* out,
                       const float* zprop, const float* pe_prop, float* zprop_next, const amh_collect* collect,

@@ -5,7 +5,8 @@ bit-identical to the oracle's) the transitions must equal orc_step bit for
 bit -- single launches, in-place multi-step runs and thinned collection --
 at d where the fused Gaussian kernel's lane group is the external path's
 (32 for 17 <= d <= 32, 64 above; d = 64's fused kernel is the step64
-specialisation, bit-identical to the generic one).  A potential written in torch samples its target."""
+specialisation, bit-identical to the generic one); above d = 64 the large-d
+propose / step passes take the caller's U as they take the MFMA potential's.  A potential written in torch samples its target."""
 import math
 
 import numpy as np
@@ -30,7 +31,7 @@ def _pair(d, C, gpu, orc, W=4, seed=0):
     return ke, st, om, ost
 
 
-@pytest.mark.parametrize("d,C", [(24, 333), (32, 200), (17, 65), (48, 130), (64, 77)])
+@pytest.mark.parametrize("d,C", [(24, 333), (32, 200), (17, 65), (48, 130), (64, 77), (100, 40), (128, 33)])
 def test_external_matches_oracle_bitexact(d, C, gpu, orc):
     ke, st, om, ost = _pair(d, C, gpu, orc)
     assert_state_bitequal(st, ost, f"d={d} init")
@@ -87,7 +88,7 @@ def test_torch_potential_samples_target(gpu):
 
 def test_external_limits(gpu):
     """What the external path does not take: sample_Pnx and ASSS (the
-    frozen / slice kernels evaluate U inside), d > 64, a potential that
+    frozen / slice kernels evaluate U inside), d > 256, a potential that
     returns the wrong number of values; NaN rejects (arwmh.py:171)."""
     from kernels_amd import ARWMH, ASSS, PRNGKey
     from kernels_amd._lib import AmhError
@@ -100,8 +101,8 @@ def test_external_limits(gpu):
     with pytest.raises(AmhError, match="device potential"):
         a = ASSS(potential_fn=U, num_chains=64)
         a.sample(a.init(PRNGKey(0), 0, torch.zeros(64, 4), (), {}))
-    with pytest.raises(AmhError, match="1 <= d <= 64"):
-        ARWMH(potential_fn=U, num_chains=8).init(PRNGKey(0), 0, torch.zeros(8, 70), (), {})
+    with pytest.raises(AmhError, match=r"dim must be in \[1, 256\]"):
+        ARWMH(potential_fn=U, num_chains=8).init(PRNGKey(0), 0, torch.zeros(8, 300), (), {})
     bad = ARWMH(potential_fn=lambda z: z.sum(), num_chains=8)
     with pytest.raises(ValueError, match="one each"):
         bad.init(PRNGKey(0), 0, torch.zeros(8, 4), (), {})
@@ -110,3 +111,28 @@ def test_external_limits(gpu):
     nan.sample_(s, 200)
     assert bool((s.z[:, 0] <= 0).all())  # every proposal into the NaN half was rejected
     assert math.isfinite(float(s.potential_energy.max()))
+
+
+def test_external_large_d_state_check(gpu):
+    """d > 64: amh_step_external takes only the state whose proposals the
+    handle holds the solves of (a stale state is refused, not stepped)."""
+    import ctypes
+    from kernels_amd import ARWMH, PRNGKey, _lib
+    from kernels_amd._lib import AmhError
+    from kernels_amd.arwmh import ctypes_state
+    U = lambda z: 0.5 * (z * z).sum(-1)  # noqa: E731
+    k = ARWMH(potential_fn=U, num_chains=16)
+    st = k.init(PRNGKey(0), 0, torch.zeros(16, 96), (), {})
+    other = k.init(PRNGKey(1), 0, torch.zeros(16, 96), (), {})
+    zp = torch.empty(16, 96, device=st.z.device)
+    L = _lib.lib()
+    s = _lib.stream_ptr(st.z.device.index)
+    _lib.check(L.amh_propose(k._handle.h, 16, ctypes_state(k, st), _lib.ptr(zp), s), k._handle.h)
+    pe = U(zp).contiguous()
+    rc = L.amh_step_external(k._handle.h, 16, ctypes_state(k, other), ctypes_state(k, other), _lib.ptr(zp),
+                             _lib.ptr(pe), None, None, s)
+    with pytest.raises(AmhError, match="proposals of this state"):
+        _lib.check(rc, k._handle.h)
+    _lib.check(L.amh_step_external(k._handle.h, 16, ctypes_state(k, st), ctypes_state(k, st), _lib.ptr(zp),
+                                   _lib.ptr(pe), None, None, s), k._handle.h)
+    assert int(st.i[0]) == 1

@@ -126,4 +126,4 @@ def test_callable_potential_becomes_external():
     with pytest.raises(TypeError):
         ARWMH(potential_fn=3.0)
     with pytest.raises(ValueError):
-        P.torch_potential(lambda z: z, dim=65)
+        P.torch_potential(lambda z: z, dim=257)
