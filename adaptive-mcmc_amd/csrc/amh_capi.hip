@@ -564,6 +564,46 @@ int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, co
   return AMH_OK;
 }
 
+static int pnx_ext(amh_handle* h, const uint32_t key[2], float* z, float* pe, int64_t C, const float* scale,
+                   float lam, int32_t t, float* zprop, const float* pe_prop, bool accept, void* stream,
+                   const char* who) {
+  if (!h) return fail(nullptr, AMH_EINVAL, std::string(who) + ": null handle");
+  if (h->model_id != AMH_MODEL_EXTERNAL) return fail(h, AMH_EINVAL, std::string(who) + ": needs AMH_MODEL_EXTERNAL");
+  if (h->cfg.dim > 64) return fail(h, AMH_EINVAL, std::string(who) + ": an external sample_Pnx needs d <= 64");
+  if (!key || !z || !zprop || C < 1 || t < 0 || (accept ? (!pe || !pe_prop) : !scale))
+    return fail(h, AMH_EINVAL, std::string(who) + ": bad arguments");
+  hipError_t e = hipSetDevice(h->device);
+  if (e != hipSuccess) return hip_fail(h, e, (std::string(who) + "/hipSetDevice").c_str());
+  amh::PnxExtParams p{};
+  p.z = z;
+  p.pe = pe;
+  p.zprop = zprop;
+  p.pe_prop = pe_prop;
+  p.C = C;
+  p.scale = scale;
+  p.log_step_size = lam;
+  p.eps = h->cfg.eps;
+  p.t = t;
+  p.d = h->cfg.dim;
+  p.key0 = key[0];
+  p.key1 = key[1];
+  e = amh::run_pnx_ext(p, accept, (hipStream_t)stream);
+  if (e != hipSuccess) return hip_fail(h, e, who);
+  return AMH_OK;
+}
+
+int amh_pnx_propose(amh_handle* h, const uint32_t key[2], const float* z, int64_t num_chains,
+                    const float* scale_packed, float log_step_size, int32_t t, float* zprop, void* stream) {
+  return pnx_ext(h, key, const_cast<float*>(z), nullptr, num_chains, scale_packed, log_step_size, t, zprop, nullptr,
+                 false, stream, "amh_pnx_propose");
+}
+
+int amh_pnx_accept(amh_handle* h, const uint32_t key[2], float* z, float* pe, int64_t num_chains,
+                   const float* zprop, const float* pe_prop, int32_t t, void* stream) {
+  return pnx_ext(h, key, z, pe, num_chains, nullptr, 0.0f, t, const_cast<float*>(zprop), pe_prop, true, stream,
+                 "amh_pnx_accept");
+}
+
 int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t n_points, int64_t n_samples,
                    const float* loc, const float* scale_packed, float log_step_size, int32_t n, float* out,
                    void* stream) {
@@ -575,7 +615,7 @@ int amh_sample_pnx(amh_handle* h, const uint32_t key[2], const float* x, int64_t
   if (h->cfg.dim > 64 && !amh::big_model(h->model_id, h->cfg.dim))
     return fail(h, AMH_EINVAL, "amh_sample_pnx: d > 64 needs the dense Gaussian (d <= 256)");
   if (h->model_id == AMH_MODEL_EXTERNAL)
-    return fail(h, AMH_EINVAL, "amh_sample_pnx: the frozen kernel needs a device potential (not external)");
+    return fail(h, AMH_EINVAL, "amh_sample_pnx: an external potential runs through amh_pnx_propose / amh_pnx_accept");
   hipError_t e = hipSetDevice(h->device);
   if (e != hipSuccess) return hip_fail(h, e, "amh_sample_pnx/hipSetDevice");
   amh::PnxParams p{};

@@ -200,6 +200,20 @@ hipError_t run_lse_rows(const float* Cm, int64_t rows, int64_t cols, const float
 hipError_t run_init(int model_id, const InitParams& p, hipStream_t s);
 hipError_t run_potential(int model_id, const PotParams& p, hipStream_t s);
 hipError_t run_pnx(int model_id, const PnxParams& p, hipStream_t s);
+// sample_Pnx with the caller's potential (AMH_MODEL_EXTERNAL, d <= 64): one
+// step t of every chain in two launches around the caller's U
+struct PnxExtParams {
+  float* z;              // [C][d] current points (accept: updated)
+  float* pe;             // [C] their U (accept: updated)
+  float* zprop;          // [C][d] proposals (propose: written)
+  const float* pe_prop;  // [C] U(zprop) (accept)
+  int64_t C;
+  const float* scale;    // shared packed factor
+  float log_step_size, eps;
+  int32_t t, d;
+  uint32_t key0, key1;
+};
+hipError_t run_pnx_ext(const PnxExtParams& p, bool accept, hipStream_t s);
 // large dimensions (64 < d <= 256, Gaussian; amh_big.hip)
 struct BigParams {
   amh_state in, out;

@@ -1734,6 +1734,71 @@ hipError_t launch_pot(const PotParams& p, hipStream_t s) {
   return hipGetLastError();
 }
 
+// sample_pnx_kernel's step t split around the caller's potential
+// (AMH_MODEL_EXTERNAL): ACCEPT = false forms every chain's proposal from the
+// shared factor (the same fmaf chain over j as sample_pnx_kernel), ACCEPT =
+// true takes U(z') from memory and applies the test with the step's u
+template <int G, bool ACCEPT>
+__global__ __launch_bounds__(kBlock) void pnx_ext_kernel(PnxExtParams p) {
+  using Gp = Grp<G>;
+  const int d = p.d;
+  const int r = Gp::r();
+  const bool act = r < d;
+  const int64_t C = p.C;
+  const int64_t n_items = (C + Geo<G>::CPW - 1) / Geo<G>::CPW;
+  const int64_t wave0 = (int64_t)blockIdx.x * (kBlock / 64) + threadIdx.x / 64;
+  const int64_t wstride = (int64_t)gridDim.x * (kBlock / 64);
+  float A[G];
+  if constexpr (!ACCEPT) {
+    static_for<G>([&](auto J) {
+      constexpr int j = J;
+      A[j] = (j < d && r >= j && act) ? p.scale[col_off(d, j) + (r - j)] : 0.0f;
+    });
+  }
+  const float el = amh_expf(p.log_step_size);
+  for (int64_t item = wave0; item < n_items; item += wstride) {
+    const int64_t chain = item_chain<G>(item);
+    const bool chain_ok = chain < C;
+    const int64_t cl = chain_ok ? chain : C - 1;
+    const amh_u32x4 kk = amh_philox4x32_10((uint32_t)cl, (uint32_t)((uint64_t)cl >> 32), 0u, AMH_TAG_SPLIT,
+                                           p.key0, p.key1);
+    const float z = act ? p.z[cl * d + r] : 0.0f;
+    if constexpr (!ACCEPT) {
+      float xi, u;
+      step_noise<G>(r, d, (uint32_t)p.t, kk.v[0], kk.v[1], xi, u);
+      xi = act ? xi : 0.0f;
+      float acc = 0.0f;
+      static_for<G>([&](auto J) {
+        if (J < d) acc = fmaf(A[J], Gp::template bcast<J>(xi), acc);
+      });
+      const float zp = act ? z + fmaf(el, acc, p.eps * xi) : 0.0f;
+      if (chain_ok && act) p.zprop[cl * d + r] = zp;
+    } else {
+      const float u = amh_unif01_from_bits(amh_step_word((uint32_t)d, (uint32_t)p.t, kk.v[0], kk.v[1]));  // W_d
+      const float pe = p.pe[cl];
+      float pep = p.pe_prop[cl];
+      if (amh_isnan(pep)) pep = INFINITY;
+      const float ex = amh_expf(pe - pep);
+      const float alpha = (ex > 1.0f) ? 1.0f : ex;
+      if (u < alpha && chain_ok) {  // group-uniform: one chain per group
+        if (act) p.z[cl * d + r] = p.zprop[cl * d + r];
+        if (r == 0) p.pe[cl] = pep;
+      }
+    }
+  }
+}
+
+hipError_t run_pnx_ext(const PnxExtParams& p, bool accept, hipStream_t s) {
+  if (p.d < 1 || p.d > 64 || p.C < 1) return hipErrorInvalidValue;
+  auto go = [&](auto kern, int64_t cpw) {
+    const int64_t n_items = (p.C + cpw - 1) / cpw;
+    hipLaunchKernelGGL(kern, dim3(grid_for(n_items, kBlock / 64)), dim3(kBlock), 0, s, p);
+    return hipGetLastError();
+  };
+  if (p.d <= 32) return accept ? go(pnx_ext_kernel<32, true>, Geo<32>::CPW) : go(pnx_ext_kernel<32, false>, Geo<32>::CPW);
+  return accept ? go(pnx_ext_kernel<64, true>, Geo<64>::CPW) : go(pnx_ext_kernel<64, false>, Geo<64>::CPW);
+}
+
 template <int DMAX, template <int> class M, bool EXACT>
 hipError_t launch_pnx(const PnxParams& p, hipStream_t s) {
   const int64_t n_items = (p.n_points * p.n_samples + Geo<DMAX>::CPW - 1) / Geo<DMAX>::CPW;

@@ -33,7 +33,7 @@ EXPORTS = ("amh_version", "amh_last_error", "amh_create", "amh_destroy", "amh_bi
            "amh_pooled_step_k", "amh_asss_step",
            "amh_asss_sample_pnx", "amh_kernel_sum_scratch", "amh_kernel_sum", "amh_pairwise_dist2",
            "amh_normals", "amh_sinkhorn_lse", "amh_check_device", "amh_pooled_allreduce", "amh_propose",
-           "amh_step_external")
+           "amh_step_external", "amh_pnx_propose", "amh_pnx_accept")
 
 
 class AmhConfig(ctypes.Structure):
@@ -104,6 +104,10 @@ def lib():
     L.amh_step_external.argtypes = [P, I64, ctypes.POINTER(AmhState), ctypes.POINTER(AmhState), P, P, P,
                                     ctypes.POINTER(AmhCollect), P]
     L.amh_step_external.restype = ctypes.c_int
+    L.amh_pnx_propose.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, I64, P, F, I32, P, P]
+    L.amh_pnx_propose.restype = ctypes.c_int
+    L.amh_pnx_accept.argtypes = [P, ctypes.POINTER(ctypes.c_uint32), P, P, I64, P, P, I32, P]
+    L.amh_pnx_accept.restype = ctypes.c_int
     L.amh_asss_sample_pnx.restype = ctypes.c_int
     L.amh_kernel_sum_scratch.argtypes = [I64, I64]
     L.amh_kernel_sum_scratch.restype = I64

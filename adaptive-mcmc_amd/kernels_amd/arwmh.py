@@ -398,12 +398,34 @@ class ARWMH:
         loc_t = torch.as_tensor(loc.cpu() if hasattr(loc, "cpu") else np.asarray(loc), dtype=torch.float32)
         loc_t = loc_t.reshape(-1)[:self._dim].to(dev).contiguous()
         lam = float(np.asarray(lam.cpu() if hasattr(lam, "cpu") else lam).reshape(-1)[0])
+        if self._external():
+            return self._sample_pnx_external(rng_key, x, scale, lam, int(n), int(n_samples), dev)
         out = torch.empty(x.shape[0], n_samples, self._dim, dtype=torch.float32, device=dev)
         with torch.cuda.device(dev.index):
             _lib.check(_lib.lib().amh_sample_pnx(self._handle.h, _lib.key_arr(as_key(rng_key)), _lib.ptr(x),
                                                  x.shape[0], n_samples, _lib.ptr(loc_t), _lib.ptr(scale), lam, n,
                                                  _lib.ptr(out), _lib.stream_ptr(dev.index)), self._handle.h)
         return out
+
+    def _sample_pnx_external(self, rng_key, x, scale, lam, n, n_samples, dev):
+        """sample_Pnx with the caller's potential: every step t is
+        amh_pnx_propose, U of the proposals, amh_pnx_accept (include/amh.h)."""
+        d, npts = self._dim, x.shape[0]
+        C = npts * n_samples
+        z = x.repeat_interleave(n_samples, dim=0).contiguous()  # chain p * n_samples + s starts at x[p]
+        zp = torch.empty_like(z)
+        key = _lib.key_arr(as_key(rng_key))
+        L = _lib.lib()
+        with torch.cuda.device(dev.index):
+            st = _lib.stream_ptr(dev.index)
+            pe = self._potential_fn.evaluate(z)
+            for t in range(n):
+                _lib.check(L.amh_pnx_propose(self._handle.h, key, _lib.ptr(z), C, _lib.ptr(scale), lam, t,
+                                             _lib.ptr(zp), st), self._handle.h)
+                pp = self._potential_fn.evaluate(zp)
+                _lib.check(L.amh_pnx_accept(self._handle.h, key, _lib.ptr(z), _lib.ptr(pe), C, _lib.ptr(zp),
+                                            _lib.ptr(pp), t, st), self._handle.h)
+        return z.reshape(npts, n_samples, d)
 
     def get_init_adapt_state(self, rng_key, init_params, model_args=(), model_kwargs={}):
         """arwmh.py:272-276."""

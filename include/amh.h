@@ -173,6 +173,19 @@ int amh_step_external(amh_handle* h, int64_t num_chains, const amh_state* in, co
                       const float* zprop, const float* pe_prop, float* zprop_next, const amh_collect* collect,
                       void* stream);
 
+/* ARWMH.sample_Pnx (arwmh.py:230-270) with AMH_MODEL_EXTERNAL, d <= 64: step
+ * t of every chain c (key split(key)[c], as amh_sample_pnx) in two calls
+ * around the caller's U.  The caller starts z[C][d] at the points (chain
+ * p * n_samples + s at x[p]) and pe[C] = U(z); per step t = 0..n-1:
+ * amh_pnx_propose writes zprop from z and the shared (scale_packed,
+ * log_step_size), the caller evaluates pe_prop = U(zprop), amh_pnx_accept
+ * moves accepted chains (u < min(1, exp(pe - pe_prop)), NaN -> +inf) into z,
+ * pe.  Same bits as amh_sample_pnx given the same U. */
+int amh_pnx_propose(amh_handle* h, const uint32_t key[2], const float* z, int64_t num_chains,
+                    const float* scale_packed, float log_step_size, int32_t t, float* zprop, void* stream);
+int amh_pnx_accept(amh_handle* h, const uint32_t key[2], float* z, float* pe, int64_t num_chains,
+                   const float* zprop, const float* pe_prop, int32_t t, void* stream);
+
 /* potential_fn(z) for n points: pe[n] from z[n][d] (arwmh.py:121). */
 int amh_potential(amh_handle* h, const float* z, float* pe, int64_t n, void* stream);
 

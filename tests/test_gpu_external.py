@@ -87,17 +87,14 @@ def test_torch_potential_samples_target(gpu):
 
 
 def test_external_limits(gpu):
-    """What the external path does not take: sample_Pnx and ASSS (the
-    frozen / slice kernels evaluate U inside), d > 256, a potential that
+    """What the external path does not take: ASSS (the slice kernel
+    evaluates U inside), d > 256, a potential that
     returns the wrong number of values; NaN rejects (arwmh.py:171)."""
     from kernels_amd import ARWMH, ASSS, PRNGKey
     from kernels_amd._lib import AmhError
     U = lambda z: 0.5 * (z * z).sum(-1)  # noqa: E731
     k = ARWMH(potential_fn=U, num_chains=64)
     st = k.init(PRNGKey(0), 0, torch.zeros(64, 4), (), {})
-    with pytest.raises(AmhError, match="device potential"):
-        k.sample_Pnx(PRNGKey(1), torch.zeros(2, 4), (st.adapt_state.loc[0], st.adapt_state.scale[0],
-                                                     st.adapt_state.log_step_size[0]), n=1, n_samples=4)
     with pytest.raises(AmhError, match="device potential"):
         a = ASSS(potential_fn=U, num_chains=64)
         a.sample(a.init(PRNGKey(0), 0, torch.zeros(64, 4), (), {}))
@@ -136,3 +133,26 @@ def test_external_large_d_state_check(gpu):
     _lib.check(L.amh_step_external(k._handle.h, 16, ctypes_state(k, st), ctypes_state(k, st), _lib.ptr(zp),
                                    _lib.ptr(pe), None, None, s), k._handle.h)
     assert int(st.i[0]) == 1
+
+
+@pytest.mark.parametrize("d", [5, 24, 48])
+def test_external_sample_pnx_bitexact(d, gpu, orc):
+    """sample_Pnx with the caller's U (amh_pnx_propose / amh_pnx_accept):
+    with U = the library's own Gaussian potential, bit for bit the oracle's
+    orc_sample_pnx (the fused frozen kernel's spec), start points included."""
+    from kernels_amd import ARWMH, PRNGKey
+    kw, mk, om = make_case("gaussian", d)
+    kg = ARWMH(num_chains=8, **kw)
+    z0 = np.random.default_rng(0).uniform(-2, 2, size=(8, d)).astype(np.float32)
+    st = kg.init(PRNGKey(1), 0, torch.as_tensor(z0), (), mk)
+    st = kg.sample_(st, 30)
+    ad = st.adapt_state
+    ke = ARWMH(potential_fn=lambda z: kg.potential(z), num_chains=8)
+    ke.init(PRNGKey(1), 0, torch.as_tensor(z0), (), {})
+    x = np.random.default_rng(3).normal(size=(4, d)).astype(np.float32)
+    out = ke.sample_Pnx(PRNGKey(7), x, (ad.loc[2], ad.scale[2], ad.log_step_size[2]), n=6, n_samples=33)
+    ref = orc.sample_pnx(om, PRNGKey(7), x, ad.loc[2].cpu().numpy(), ad.scale[2].cpu().numpy(),
+                         float(ad.log_step_size[2].cpu()), 6, 33)
+    assert out.shape == (4, 33, d)
+    np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
+    assert np.mean(np.any(ref != x[:, None, :], axis=-1)) > 0.2
