@@ -1,7 +1,9 @@
 """ARWMH sample() per launch at large d (regime A: per-chain adaptation; the
 step pass chains the next proposal), correlated Gaussian with kappa = 1e4 as
 BASELINE configs[3]: ms per launch over 100 launches after 50 warm-up
-launches (HIP events).  Usage: python3 tools/big_run.py [C] [d]"""
+launches (HIP events).  Usage: python3 tools/big_run.py [C] [d] [nochain]
+(nochain: every sample() runs the propose pass instead of taking the step
+pass's next proposal)"""
 import os
 import sys
 
@@ -15,6 +17,7 @@ from kernels_amd import ARWMH, PRNGKey  # noqa: E402
 C = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 d = int(sys.argv[2]) if len(sys.argv) > 2 else 256
 k = ARWMH(potential_fn=P.correlated_gaussian(d, log10_kappa=4.0), num_chains=C)
+k.chain_proposals = not (len(sys.argv) > 3 and sys.argv[3] == "nochain")
 st = k.init(PRNGKey(0), 0, (torch.rand(C, d, device="cuda") * 4 - 2).contiguous(), (), {})
 for _ in range(50):
     st = k.sample(st, (), {})
@@ -27,4 +30,4 @@ b.record()
 torch.cuda.synchronize()
 ms = a.elapsed_time(b) / 100
 lib = os.path.basename(os.path.dirname(os.environ.get("AMH_LIB_PATH", "release/x")))
-print(f"arwmh {lib} C={C} d={d}: {ms:.4f} ms per sample(), {C / ms * 1e3:.4g} chain-steps/s", flush=True)
+print(f"arwmh {lib}{'' if k.chain_proposals else ' nochain'} C={C} d={d}: {ms:.4f} ms per sample(), {C / ms * 1e3:.4g} chain-steps/s", flush=True)
