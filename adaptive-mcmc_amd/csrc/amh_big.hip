@@ -135,7 +135,7 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
         // register is copied while its read is in flight)
         float vn[NS];
         rd(0, vn);
-        lds_wait_n(vn);
+        if constexpr (NS == 3) { lds_wait(vn[0], vn[1], vn[2]); } else { lds_wait_n(vn); }
         // RAG (d % 8 != 0): a run-time column count for the ragged last
         // block; the aligned instantiation keeps the compile-time trip count
         // (a run-time bound in it cost 12-17 % at d = 256)
@@ -150,7 +150,7 @@ __device__ __forceinline__ void for_columns(const float* Lc, int d, int64_t P, f
           if (q + 1 < qn) rd(q + 1, vn);
           f(KB, kColBlk * b + q, v);
 #endif
-          lds_wait_n(vn);
+          if constexpr (NS == 3) { lds_wait(vn[0], vn[1], vn[2]); } else { lds_wait_n(vn); }
         }
       }
     }
@@ -1138,6 +1138,12 @@ bool pooled_big_model(int model_id, int d) {
   return model_id == AMH_MODEL_GAUSSIAN && d >= 64 && d <= 256 && d % 32 == 0;
 }
 
+// row slots per lane by d: two up to 128, three up to 192, four up to 256
+// (each a separate instantiation; big_sum adds the absent slots as +0)
+#ifndef AMH_BIG_NS3
+#define AMH_BIG_NS3 1
+#endif
+static int row_slots(int d) { return d <= 128 ? 2 : ((AMH_BIG_NS3 && d <= 192) ? 3 : 4); }
 static int wave_grid(int64_t n) {
   int64_t b = (n + 3) / 4;
   if (b > 256 * 16) b = 256 * 16;
@@ -1145,45 +1151,47 @@ static int wave_grid(int64_t n) {
 }
 
 hipError_t run_big_init(const InitParams& p, hipStream_t s) {
-  auto k = (p.d <= 128) ? big_init_kernel<2> : big_init_kernel<4>;
+  const int ns = row_slots(p.d);
+  auto k = ns == 2 ? big_init_kernel<2> : (ns == 3 ? big_init_kernel<3> : big_init_kernel<4>);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), 0, s, p);
   return hipGetLastError();
 }
 static size_t stream_lds(int d) { return (size_t)4 * 2 * kColBlk * d * sizeof(float); }
+#define AMH_BY_NS(NAME, ...) \
+  (ns == 2 ? NAME<__VA_ARGS__, 2> : (ns == 3 ? NAME<__VA_ARGS__, 3> : NAME<__VA_ARGS__, 4>))
 hipError_t run_big_propose(const BigParams& p, hipStream_t s) {
-  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
-  auto k = rag ? (two ? big_propose_kernel<true, 2> : big_propose_kernel<true, 4>)
-               : (two ? big_propose_kernel<false, 2> : big_propose_kernel<false, 4>);
+  const bool rag = p.d % kColBlk != 0;
+  const int ns = row_slots(p.d);
+  auto k = rag ? AMH_BY_NS(big_propose_kernel, true) : AMH_BY_NS(big_propose_kernel, false);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_step(const BigParams& p, hipStream_t s, bool next) {
-  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
-  auto k = next ? (rag ? (two ? big_step_kernel<true, true, 2> : big_step_kernel<true, true, 4>)
-                       : (two ? big_step_kernel<true, false, 2> : big_step_kernel<true, false, 4>))
-                : (rag ? (two ? big_step_kernel<false, true, 2> : big_step_kernel<false, true, 4>)
-                       : (two ? big_step_kernel<false, false, 2> : big_step_kernel<false, false, 4>));
+  const bool rag = p.d % kColBlk != 0;
+  const int ns = row_slots(p.d);
+  auto k = next ? (rag ? AMH_BY_NS(big_step_kernel, true, true) : AMH_BY_NS(big_step_kernel, true, false))
+                : (rag ? AMH_BY_NS(big_step_kernel, false, true) : AMH_BY_NS(big_step_kernel, false, false));
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_step(const StepParams& p, hipStream_t s) {
-  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
-  auto k = rag ? (two ? asss_big_step_kernel<true, 2> : asss_big_step_kernel<true, 4>)
-               : (two ? asss_big_step_kernel<false, 2> : asss_big_step_kernel<false, 4>);
+  const bool rag = p.d % kColBlk != 0;
+  const int ns = row_slots(p.d);
+  auto k = rag ? AMH_BY_NS(asss_big_step_kernel, true) : AMH_BY_NS(asss_big_step_kernel, false);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.C)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_big_pnx(const PnxParams& p, hipStream_t s) {
-  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
-  auto k = rag ? (two ? big_pnx_kernel<true, 2> : big_pnx_kernel<true, 4>)
-               : (two ? big_pnx_kernel<false, 2> : big_pnx_kernel<false, 4>);
+  const bool rag = p.d % kColBlk != 0;
+  const int ns = row_slots(p.d);
+  auto k = rag ? AMH_BY_NS(big_pnx_kernel, true) : AMH_BY_NS(big_pnx_kernel, false);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }
 hipError_t run_asss_big_pnx(const AsssPnxParams& p, hipStream_t s) {
-  const bool rag = p.d % kColBlk != 0, two = p.d <= 128;
-  auto k = rag ? (two ? asss_big_pnx_kernel<true, 2> : asss_big_pnx_kernel<true, 4>)
-               : (two ? asss_big_pnx_kernel<false, 2> : asss_big_pnx_kernel<false, 4>);
+  const bool rag = p.d % kColBlk != 0;
+  const int ns = row_slots(p.d);
+  auto k = rag ? AMH_BY_NS(asss_big_pnx_kernel, true) : AMH_BY_NS(asss_big_pnx_kernel, false);
   hipLaunchKernelGGL(k, dim3(wave_grid(p.n_points * p.n_samples)), dim3(256), stream_lds(p.d), s, p);
   return hipGetLastError();
 }

@@ -54,7 +54,8 @@ def _init(kind, C, orc, seed=0, d=None, num_warmup=0):
                                       # large d (amh_big.hip asss_big_step_kernel, round 5)
                                       ("gaussian", 96, 130), ("gaussian", 128, 100), ("gaussian", 256, 70),
                                       # any 64 < d <= 256 (round 6): ragged tile / dword DMA / odd d
-                                      ("gaussian", 72, 90), ("gaussian", 100, 77), ("gaussian", 97, 65)])
+                                      ("gaussian", 72, 90), ("gaussian", 100, 77), ("gaussian", 97, 65),
+                                      ("gaussian", 160, 50), ("gaussian", 150, 40)])
 def test_asss_single_steps_bitexact(kind, d, C, gpu, orc):
     """ASSS.sample (one launch per step, out of place) vs oracle, 25 steps."""
     k, st, om, ost = _init(kind, C, orc, d=d, num_warmup=8)

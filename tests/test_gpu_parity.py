@@ -113,7 +113,8 @@ def test_split_path_generic_k(gpu, orc):
     np.testing.assert_array_equal(pe.view(np.uint32), orc.potential(om, z).view(np.uint32))
 
 
-@pytest.mark.parametrize("d,C,steps", [(128, 77, 12), (256, 33, 6), (72, 70, 8), (100, 65, 8), (97, 41, 8)])
+@pytest.mark.parametrize("d,C,steps", [(128, 77, 12), (256, 33, 6), (72, 70, 8), (100, 65, 8), (97, 41, 8),
+                                        (160, 40, 6), (150, 33, 5), (192, 30, 5)])
 def test_big_dim_bitexact(d, C, steps, gpu, orc):
     """64 < d <= 256 (amh_big.hip: propose pass, MFMA potential, step pass):
     init, single launches (gamma_1 = 1 keep-L at step 1, the warmup reset at
@@ -149,7 +150,7 @@ def test_sample_pnx_bitexact(gpu, orc):
     np.testing.assert_array_equal(out.cpu().numpy().view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("d", [96, 128, 256, 100, 97])
+@pytest.mark.parametrize("d", [96, 128, 256, 100, 97, 160, 150])
 def test_sample_pnx_large_d_bitexact(d, gpu, orc):
     """ARWMH.sample_Pnx at 64 < d <= 256 (big_pnx_kernel: the shared factor
     streamed per step, U by P's rows in the MFMA potential's order) against
